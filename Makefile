@@ -1,0 +1,20 @@
+# Build the product library (HIP, gfx950) and the CPU oracle (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -shared -Wall -Wno-unused-function
+SRC := p265_amd/csrc/p265r.hip
+HDR := $(wildcard p265_amd/csrc/*.h) include/p265r.h
+
+all: p265_amd/libp265r.so
+
+p265_amd/libp265r.so: $(SRC) $(HDR)
+	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f p265_amd/libp265r.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

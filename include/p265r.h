@@ -1,0 +1,169 @@
+/*
+ * p265r.h -- C ABI of the MI355X (gfx950) HEVC intra reconstruction back-end.
+ *
+ * Drop-in boundary for the reconstruction hook of the p265 reference decoder.
+ * The reference has no FFI: its boundary is the Python call
+ *     Cu.parse -> Cu.decode_leaf()                 (decoder/cu.py:96-97, cu.py:483-494)
+ * which (were it not dead, cu.py:487-488) would run, per leaf CU,
+ *     Cu.decode_intra -> IntraPu.decode            (cu.py:595-615, intra.py:39-70)
+ *       -> scaling.inverse_scaling                 (scaling.py:4-47)
+ *       -> transform.inverse_transform             (transform.py:89-109)
+ *       -> reconstruction.reconstruction           (reconstruction.py:4-27)
+ * with the picture served back through Cu.get_reconstructed_sample (cu.py:617-632),
+ * and the per-CTU SAO syntax of Sao.parse (sao.py:15-136) that nothing consumes.
+ *
+ * Here decode_leaf() only APPENDS records (one p265r_tb per transform block, one
+ * p265r_ctu per CTU); at end of picture (slice.py:284-286) the host submits a batch
+ * of pictures; the device runs dequant + inverse DCT/DST + intra prediction +
+ * reconstruction + SAO and writes the decoded planes.  See INTEGRATION.md for the
+ * ctypes binding the reference would add.
+ *
+ * Conventions: every function returns int (0 = P265R_OK, < 0 = error code, see
+ * p265r_strerror); no exception or C++ type crosses this boundary.  All host
+ * buffers are owned by the caller.  A context is bound to one device and is not
+ * thread-safe: use one context per GPU per thread/process.
+ */
+#ifndef P265R_H
+#define P265R_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P265R_ABI_VERSION 1u
+
+/* error codes */
+#define P265R_OK            0
+#define P265R_EINVAL       -1   /* bad argument / malformed record              */
+#define P265R_ENOMEM       -2   /* host or device allocation failed             */
+#define P265R_EHIP         -3   /* HIP runtime error (see p265r_last_hip_error) */
+#define P265R_EUNSUPPORTED -4   /* stream feature outside this back-end's scope */
+#define P265R_ERANGE       -5   /* record points outside picture / buffers      */
+#define P265R_ESTATE       -6   /* call out of order (e.g. wait without submit) */
+#define P265R_ENODEV       -7   /* no such HIP device                           */
+
+/* p265r_tb.flags */
+#define P265R_TB_CBF     0x01u  /* coefficients present at coef_off (N*N int16, raster)        */
+#define P265R_TB_TSKIP   0x02u  /* transform_skip_flag (tu.py:142-143)                        */
+#define P265R_TB_BYPASS  0x04u  /* cu_transquant_bypass_flag (cu.py:102-105)                 */
+#define P265R_TB_PCM     0x08u  /* PCM block: coef holds samples at BitDepth; no prediction    */
+
+/* p265r_ctu.flags */
+#define P265R_CTU_LF_ACROSS_SLICES 0x01u  /* slice_loop_filter_across_slices_enabled_flag of its slice */
+
+/* Sequence-level parameters (SPS/PPS-derived fields the path reads; sps.py:59-62,
+ * sps.py:142-171, sps.py:120, pps.py:38).  POD, 32 bytes: RCCL-broadcastable. */
+typedef struct p265r_params {
+    uint32_t version;                 /* = P265R_ABI_VERSION                      */
+    uint16_t pic_width;               /* pic_width_in_luma_samples                */
+    uint16_t pic_height;              /* pic_height_in_luma_samples               */
+    uint8_t  chroma_format_idc;       /* 1 (4:2:0) only                           */
+    uint8_t  bit_depth_luma;          /* 8 only in this version                   */
+    uint8_t  bit_depth_chroma;        /* 8 only in this version                   */
+    uint8_t  ctb_log2_size;           /* CtbLog2SizeY, 4..6                       */
+    uint8_t  min_tb_log2_size;        /* MinTbLog2SizeY, 2..5                     */
+    uint8_t  max_tb_log2_size;        /* MaxTbLog2SizeY, <= 5                     */
+    uint8_t  strong_intra_smoothing;  /* strong_intra_smoothing_enabled_flag      */
+    uint8_t  constrained_intra_pred;  /* constrained_intra_pred_flag (no effect: all-intra) */
+    uint8_t  sample_adaptive_offset;  /* sample_adaptive_offset_enabled_flag      */
+    uint8_t  loop_filter_across_tiles;/* loop_filter_across_tiles_enabled_flag    */
+    uint8_t  scaling_list_enabled;    /* must be 0 in this version                */
+    uint8_t  reserved[13];
+} p265r_params;
+
+/* One CTU, raster order, PicSizeInCtbsY per picture.  32 bytes. */
+typedef struct p265r_ctu {
+    uint32_t tb_begin;        /* first p265r_tb of this CTU (its TBs are contiguous, decode order) */
+    uint16_t tb_count;
+    uint16_t tile_id;         /* TileId (tiles numbered in tile-scan order)                    */
+    uint32_t slice_addr;      /* SliceAddrRs of the slice containing this CTU                  */
+    uint8_t  flags;           /* P265R_CTU_*                                                   */
+    uint8_t  sao_type[3];     /* SaoTypeIdx[cIdx]: 0 off, 1 band offset, 2 edge offset         */
+    uint8_t  sao_class[3];    /* sao_band_position (type 1) or SaoEoClass (type 2)             */
+    uint8_t  reserved;
+    int8_t   sao_offset[3][4];/* SaoOffsetVal[cIdx][1..4]: signed, << log2OffsetScale          */
+} p265r_ctu;
+
+/* One transform block, in decode order within its CTU.  16 bytes.
+ * Luma TBs of a TU precede its Cb and Cr TBs; for a luma 4x4 quad the single
+ * 4x4 Cb/Cr pair follows blkIdx 3 (tu.py:127-135). */
+typedef struct p265r_tb {
+    uint16_t x, y;            /* top-left, in samples of component c_idx                       */
+    uint8_t  log2_size;       /* 2..5                                                          */
+    uint8_t  c_idx;           /* 0 Y, 1 Cb, 2 Cr                                               */
+    uint8_t  pred_mode;       /* IntraPredModeY / IntraPredModeC, 0..34                        */
+    uint8_t  flags;           /* P265R_TB_*                                                    */
+    uint8_t  qp;              /* qP for scaling: Qp'Y or Qp'Cb / Qp'Cr (incl. QpBdOffset)      */
+    uint8_t  reserved[3];
+    uint32_t coef_off;        /* int16 offset of the N*N TransCoeffLevel[y][x] (iff CBF|PCM)   */
+} p265r_tb;
+
+/* One picture of a batch (host memory, caller-owned). */
+typedef struct p265r_picture {
+    const p265r_ctu* ctus;    /* PicSizeInCtbsY entries, raster order                          */
+    const p265r_tb*  tbs;
+    uint32_t         n_tbs;
+    uint32_t         reserved0;
+    const int16_t*   coef;
+    uint64_t         n_coef;
+    const uint8_t*   nofilter;/* optional (NULL): per 8x8 luma block, raster, ceil(W/8) wide;
+                                 1 = SAO leaves the block's samples untouched
+                                 (pcm_loop_filter_disabled && pcm, or cu_transquant_bypass)   */
+    void*            out[3];  /* decoded (post-SAO) planes Y, Cb, Cr; stride = plane width;
+                                 uint8_t samples (8-bit).  NULL = do not download              */
+    void*            recon[3];/* optional pre-SAO planes, same layout; NULL = skip             */
+} p265r_picture;
+
+/* Per-phase device time of the last run, from HIP events on the context's stream. */
+typedef struct p265r_timings {
+    double   total_ms;        /* first kernel start -> last kernel end                     */
+    double   residual_ms;     /* dequant + inverse transform kernels                       */
+    double   intra_ms;        /* intra prediction + reconstruction (all wavefront steps)   */
+    double   sao_ms;          /* SAO kernel                                                */
+    int32_t  intra_launches;  /* kernel launches in the intra phase                        */
+    int32_t  residual_launches;
+    int32_t  sao_launches;
+    int32_t  reserved;
+} p265r_timings;
+
+typedef struct p265r_ctx   p265r_ctx;
+typedef struct p265r_batch p265r_batch;
+
+/* Context on HIP device `device` for a sequence with parameters `params`. */
+int  p265r_create(int device, const p265r_params* params, p265r_ctx** out);
+void p265r_destroy(p265r_ctx* ctx);
+
+/* Validate the records of n_pics pictures and copy them (plus output planes) into a
+ * device-resident batch.  Synchronous w.r.t. the host buffers. */
+int  p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p265r_batch** out);
+/* Enqueue reconstruction + SAO of every picture of the batch on the context stream. */
+int  p265r_batch_run(p265r_ctx* ctx, p265r_batch* batch);
+/* Wait for the batch and copy its planes into pics[i].out / pics[i].recon. */
+int  p265r_batch_download(p265r_ctx* ctx, p265r_batch* batch, const p265r_picture* pics, int n_pics);
+int  p265r_batch_free(p265r_ctx* ctx, p265r_batch* batch);
+
+/* Convenience: upload + run (asynchronous) ... */
+int  p265r_submit(p265r_ctx* ctx, const p265r_picture* pics, int n_pics);
+/* ... then block until outputs are written into the pictures given to submit. */
+int  p265r_wait(p265r_ctx* ctx);
+
+/* Block until the context stream is idle. */
+int  p265r_sync(p265r_ctx* ctx);
+/* Enable (1) / disable (0) per-phase HIP-event timing; read the last run's timings. */
+int  p265r_set_timing(p265r_ctx* ctx, int enable);
+int  p265r_last_timings(p265r_ctx* ctx, p265r_timings* out);
+
+/* Number of HIP devices visible (>= 0), or an error code. */
+int  p265r_device_count(void);
+const char* p265r_strerror(int code);
+/* Text of the last HIP error seen by this library (thread-local), "" if none. */
+const char* p265r_last_hip_error(void);
+/* Library ABI version (P265R_ABI_VERSION). */
+uint32_t p265r_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P265R_H */

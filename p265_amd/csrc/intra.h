@@ -1,0 +1,368 @@
+// Intra prediction + reconstruction phase: one wavefront (64 lanes) per CTU.
+//
+// Replaces the per-CU chain of the reference, Cu.decode_intra -> IntraPu.decode ->
+// decode_neighbor / decode_intra_{planar,dc,angular} -> reconstruction
+// (decoder/cu.py:595-615, decoder/intra.py:39-305, decoder/reconstruction.py:4-27),
+// which fetches every neighbour sample through a tree walk (cu.py:617-632,
+// image.py:38-73) and never runs (cu.py:487-488).
+//
+// Scheduling: intra TBs of a CTU are serial (decode order), and a CTU needs its left,
+// top-left, top and top-right CTUs.  The host launches one kernel per anti-diagonal
+// step s = cx + 2*cy (2-CTU-lag wavefront) over ALL pictures of the batch, so every
+// launch holds (CTUs on the diagonal) x (pictures) independent wavefronts.
+//
+// Per CTU the wave keeps, in LDS: the CTU's own reconstructed samples (interior),
+// the row above it (x = -1 .. 2*CtbSize-1, incl. top-left and top-right CTUs) and the
+// column left of it, all loaded once from the picture plane.  Neighbour availability
+// (6.4.1) is then decided per reference sample without any table: outside the CTU by
+// the CTU-level slice/tile checks, inside it by the z-order (Morton) rank of the 4x4
+// block, which is exactly MinTbAddrZs restricted to one CTB (pps.py:246-262).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/p265r.h"
+#include "tables.h"
+
+namespace p265r {
+
+struct DevPic {                 // per picture, device-resident table
+    const p265r_ctu* ctus;
+    const p265r_tb*  tbs;       // coef_off rewritten to pool offsets
+    uint8_t* rec[3];            // pre-SAO planes (padded stride)
+    uint8_t* out[3];            // SAO output planes (== rec when SAO is off)
+    const uint8_t* nofilter;    // per 8x8 luma block or nullptr
+};
+
+struct Geo {                    // batch-uniform geometry
+    int w, h;                   // luma size
+    int cw, ch;                 // chroma size
+    int stride[3];
+    int ctb_log2, wc, hc;
+    int bd[3];
+    int strong;
+    int lf_tiles;
+    int nf_w;                   // nofilter map width (ceil(w/8))
+};
+
+__constant__ int8_t  c_angle[35];
+__constant__ int16_t c_inv_angle[35];
+
+__device__ __forceinline__ int morton4(int x, int y) {      // 4-bit x, y -> 8-bit z-order
+    x = (x | (x << 2)) & 0x33; x = (x | (x << 1)) & 0x55;
+    y = (y | (y << 2)) & 0x33; y = (y | (y << 1)) & 0x55;
+    return x | (y << 1);
+}
+
+__device__ __forceinline__ bool ctu_same_region(const p265r_ctu& a, const p265r_ctu& b) {
+    return a.slice_addr == b.slice_addr && a.tile_id == b.tile_id;
+}
+
+struct CtuLds {
+    uint8_t  y[64 * 64];        // interior luma, stride 64
+    uint8_t  c[2][32 * 32];     // interior chroma, stride 32
+    uint8_t  ytop[132];         // row y=-1, x = -1 .. 127  (index x+1)
+    uint8_t  ctop[2][68];       // row y=-1, x = -1 .. 63
+    uint8_t  yleft[64];         // column x=-1, y = 0 .. 63
+    uint8_t  cleft[2][32];
+    uint16_t ref[2][136];       // linear reference arrays (raw/substituted, filtered)
+};
+
+// Availability of the neighbouring sample at CTB-relative LUMA position (xl, yl) for a
+// block whose top-left is at CTB-relative luma (xc, yc).  flags: bit0 L, bit1 T, bit2 TL, bit3 TR.
+__device__ __forceinline__ bool nb_available(int xl, int yl, int xc, int yc, int x0, int y0,
+                                             const Geo& g, int ctb, unsigned flags) {
+    if (x0 + xl >= g.w || y0 + yl >= g.h) return false;
+    if (yl < 0) {
+        if (xl < 0) return flags & 4u;
+        if (xl < ctb) return flags & 2u;
+        if (xl < 2 * ctb) return flags & 8u;
+        return false;
+    }
+    if (xl < 0) return (yl < ctb) && (flags & 1u);
+    if (xl >= ctb || yl >= ctb) return false;
+    return morton4(xl >> 2, yl >> 2) < morton4(xc >> 2, yc >> 2);
+}
+
+__global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict__ pics,
+                                                       const int16_t* __restrict__ pool,
+                                                       const int16_t* __restrict__ resid,
+                                                       Geo g, int step, int cy_min) {
+    __shared__ CtuLds L;
+    const int lane = threadIdx.x;
+    const int cy = cy_min + blockIdx.x;
+    const int cx = step - 2 * cy;
+    if (cy >= g.hc || cx < 0 || cx >= g.wc) return;
+    const DevPic P = pics[blockIdx.y];
+    const int ctb = 1 << g.ctb_log2;
+    const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
+    const int addr = cy * g.wc + cx;
+    const p265r_ctu me = P.ctus[addr];
+
+    unsigned flags = 0;
+    if (cx > 0 && ctu_same_region(me, P.ctus[addr - 1])) flags |= 1u;
+    if (cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc])) flags |= 2u;
+    if (cx > 0 && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc - 1])) flags |= 4u;
+    if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc + 1])) flags |= 8u;
+
+    // ---- neighbour rows/columns from the picture planes -------------------------
+    for (int c = 0; c < 3; ++c) {
+        const int sub = c ? 1 : 0;
+        const int cs = ctb >> sub;
+        const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
+        const int xb = x0 >> sub, yb = y0 >> sub;
+        const uint8_t* plane = P.rec[c];
+        const int st = g.stride[c];
+        uint8_t* top = c ? L.ctop[c - 1] : L.ytop;
+        uint8_t* left = c ? L.cleft[c - 1] : L.yleft;
+        for (int e = lane; e <= 2 * cs; e += 64) {
+            const int x = e - 1;
+            const unsigned need = x < 0 ? 4u : (x < cs ? 2u : 8u);
+            if ((flags & need) && xb + x < W) top[e] = plane[(size_t)(yb - 1) * st + xb + x];
+        }
+        if ((flags & 1u) && lane < cs && yb + lane < H) left[lane] = plane[(size_t)(yb + lane) * st + xb - 1];
+    }
+    __syncthreads();
+
+    const p265r_tb* tbs = P.tbs + me.tb_begin;
+    for (int t = 0; t < (int)me.tb_count; ++t) {
+        const p265r_tb tb = tbs[t];
+        const int c = tb.c_idx;
+        const int sub = c ? 1 : 0;
+        const int log2 = tb.log2_size, n = 1 << log2;
+        const int cs = ctb >> sub;
+        const int xr = tb.x - (x0 >> sub), yr = tb.y - (y0 >> sub);   // CTB-relative, component units
+        const int bd = g.bd[c];
+        const int maxv = (1 << bd) - 1;
+        uint8_t* interior = c ? L.c[c - 1] : L.y;
+        const int ist = c ? 32 : 64;
+        uint8_t* top = c ? L.ctop[c - 1] : L.ytop;
+        uint8_t* left = c ? L.cleft[c - 1] : L.yleft;
+
+        // samples owned by this lane: S consecutive in raster order of the TB
+        const int nn = n * n;
+        const int S = nn >= 64 ? (nn >> 6) : 1;
+        const bool own = lane * S < nn;
+        const int sidx = lane * S;
+        const int sy = sidx >> log2, sx = sidx & (n - 1);
+
+        // residual (prefetched before the reference-sample work)
+        int res[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) res[i] = 0;
+        const bool coded = tb.flags & (P265R_TB_CBF | P265R_TB_PCM);
+        if (coded && own) {
+            // residuals come from the residual phase, raw levels (bypass / PCM) from the pool
+            const int16_t* rp = ((tb.flags & (P265R_TB_BYPASS | P265R_TB_PCM)) ? pool : resid) + tb.coef_off + sidx;
+            if (S == 16) {
+                const uint4 a = *reinterpret_cast<const uint4*>(rp);
+                const uint4 b = *reinterpret_cast<const uint4*>(rp + 8);
+                const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+                for (int i = 0; i < 16; ++i) res[i] = (int)(int16_t)(w[i >> 1] >> ((i & 1) * 16));
+            } else if (S == 4) {
+                const uint2 a = *reinterpret_cast<const uint2*>(rp);
+                res[0] = (int)(int16_t)(a.x & 0xffff); res[1] = (int)(int16_t)(a.x >> 16);
+                res[2] = (int)(int16_t)(a.y & 0xffff); res[3] = (int)(int16_t)(a.y >> 16);
+            } else {
+                res[0] = rp[0];
+            }
+        }
+
+        int pred[16];
+        if (tb.flags & P265R_TB_PCM) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pred[i] = 0;
+        } else {
+            // ---- reference samples in linear order k = 0..4n --------------------
+            const int nref = 4 * n + 1;
+            int val[3];
+            bool av[3];
+            const int xcl = xr << sub, ycl = yr << sub;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int k = lane + 64 * j;
+                val[j] = 0;
+                av[j] = false;
+                if (k < nref) {
+                    const int dx = k < 2 * n ? -1 : (k == 2 * n ? -1 : k - 2 * n - 1);
+                    const int dy = k < 2 * n ? 2 * n - 1 - k : -1;
+                    const int xn = xr + dx, yn = yr + dy;
+                    av[j] = nb_available(xn << sub, yn << sub, xcl, ycl, x0, y0, g, ctb, flags);
+                    if (av[j]) {
+                        val[j] = yn < 0 ? top[xn + 1] : (xn < 0 ? left[yn] : interior[yn * ist + xn]);
+                    }
+                    L.ref[0][k] = (uint16_t)val[j];
+                }
+            }
+            const unsigned long long m0 = __ballot(av[0]);
+            const unsigned long long m1 = __ballot(av[1]);
+            const unsigned long long m2 = __ballot(av[2]);
+            __syncthreads();
+            // ---- substitution (8.4.4.2.2) -----------------------------------------
+            const bool any = (m0 | m1 | m2) != 0ull;
+            const int first = m0 ? __ffsll((long long)m0) - 1
+                                 : (m1 ? 64 + __ffsll((long long)m1) - 1 : 128 + __ffsll((long long)m2) - 1);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int k = lane + 64 * j;
+                if (k < nref && !av[j]) {
+                    int src = -1;
+                    const unsigned long long mk[3] = {m0, m1, m2};
+                    const unsigned long long below = lane ? (mk[j] & ((1ull << lane) - 1ull)) : 0ull;
+                    if (below) src = 64 * j + 63 - __clzll((long long)below);
+                    else if (j >= 2 && m1) src = 64 + 63 - __clzll((long long)m1);
+                    else if (j >= 1 && m0) src = 63 - __clzll((long long)m0);
+                    if (src < 0) src = first;
+                    val[j] = any ? (int)L.ref[0][src] : (1 << (bd - 1));
+                }
+            }
+            __syncthreads();
+            const int mode = tb.pred_mode;
+            // ---- filtering (8.4.4.2.3), luma only ---------------------------------
+            bool filt = false;
+            if (c == 0 && mode != 1 && n != 4) {
+                const int dist = min(abs(mode - 26), abs(mode - 10));
+                const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
+                filt = dist > thr;
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int k = lane + 64 * j;
+                if (k < nref) L.ref[0][k] = (uint16_t)val[j];
+            }
+            __syncthreads();
+            const uint16_t* R = L.ref[0];
+            if (filt) {
+                const int corner = R[2 * n], bl = R[0], tr = R[4 * n];
+                const bool strong = g.strong && n == 32 &&
+                                    abs(corner + tr - 2 * (int)R[3 * n]) < (1 << (bd - 5)) &&
+                                    abs(corner + bl - 2 * (int)R[n]) < (1 << (bd - 5));
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int k = lane + 64 * j;
+                    if (k < nref) {
+                        int f;
+                        if (k == 0 || k == 4 * n) f = R[k];
+                        else if (strong) {
+                            f = k == 2 * n ? corner
+                              : (k < 2 * n ? ((63 - (2 * n - 1 - k)) * corner + (2 * n - k) * bl + 32) >> 6
+                                           : ((63 - (k - 2 * n - 1)) * corner + (k - 2 * n) * tr + 32) >> 6);
+                        } else f = (R[k - 1] + 2 * R[k] + R[k + 1] + 2) >> 2;
+                        L.ref[1][k] = (uint16_t)f;
+                    }
+                }
+                __syncthreads();
+                R = L.ref[1];
+            }
+            // ---- prediction (8.4.4.2.4-6) -----------------------------------------
+            if (mode == 0) {
+                const int trs = R[3 * n + 1], bls = R[n - 1];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (i < S) {
+                        const int x = sx + i, y = sy;
+                        pred[i] = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * trs + (n - 1 - y) * R[2 * n + 1 + x] +
+                                   (y + 1) * bls + n) >> (log2 + 1);
+                    }
+                }
+            } else if (mode == 1) {
+                int s = 0;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int k = lane + 64 * j;
+                    if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) s += val[j];
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+                const int dc = (s + n) >> (log2 + 1);
+                const bool edge = c == 0 && n < 32;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (i < S) {
+                        const int x = sx + i, y = sy;
+                        int v = dc;
+                        if (edge) {
+                            if (x == 0 && y == 0) v = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
+                            else if (y == 0) v = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
+                            else if (x == 0) v = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
+                        }
+                        pred[i] = v;
+                    }
+                }
+            } else {
+                const int ang = c_angle[mode];
+                const int inv = c_inv_angle[mode];
+                const bool vert = mode >= 18;
+                const int dir = vert ? 1 : -1;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (i < S) {
+                        const int x = sx + i, y = sy;
+                        const int a = vert ? y : x, b = vert ? x : y;
+                        const int idx = ((a + 1) * ang) >> 5, fact = ((a + 1) * ang) & 31;
+                        const int r0 = b + idx + 1;
+                        const int k0 = r0 >= 0 ? 2 * n + dir * r0 : 2 * n - dir * ((r0 * inv + 128) >> 8);
+                        int v = R[k0];
+                        if (fact) {
+                            const int r1 = r0 + 1;
+                            const int k1 = r1 >= 0 ? 2 * n + dir * r1 : 2 * n - dir * ((r1 * inv + 128) >> 8);
+                            v = ((32 - fact) * v + fact * (int)R[k1] + 16) >> 5;
+                        }
+                        if (c == 0 && n < 32) {
+                            if (mode == 26 && x == 0) v = min(max((int)R[2 * n + 1] + (((int)R[2 * n - 1 - y] - (int)R[2 * n]) >> 1), 0), maxv);
+                            if (mode == 10 && y == 0) v = min(max((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), 0), maxv);
+                        }
+                        pred[i] = v;
+                    }
+                }
+            }
+        }
+        // ---- reconstruction: Clip1(pred + res) into the CTU's LDS image ------------
+        if (own) {
+            uint8_t* dst = interior + (yr + sy) * ist + xr + sx;
+            if (S == 16) {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        v |= (uint32_t)min(max(pred[q * 4 + b] + res[q * 4 + b], 0), maxv) << (8 * b);
+                    w[q] = v;
+                }
+                *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+            } else if (S == 4) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) v |= (uint32_t)min(max(pred[b] + res[b], 0), maxv) << (8 * b);
+                *reinterpret_cast<uint32_t*>(dst) = v;
+            } else {
+                dst[0] = (uint8_t)min(max(pred[0] + res[0], 0), maxv);
+            }
+        }
+        (void)cs;
+        __syncthreads();
+    }
+
+    // ---- write the CTU back to the picture planes (clipped to the picture) -----------
+    for (int c = 0; c < 3; ++c) {
+        const int sub = c ? 1 : 0;
+        const int cs = ctb >> sub;
+        const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
+        const int xb = x0 >> sub, yb = y0 >> sub;
+        const int wv = min(cs, W - xb), hv = min(cs, H - yb);
+        const uint8_t* src = c ? L.c[c - 1] : L.y;
+        const int ist = c ? 32 : 64;
+        uint8_t* plane = P.rec[c];
+        const int st = g.stride[c];
+        // 4-byte granules (plane widths are multiples of 4: MinCbSize >= 8)
+        const int gpr = wv >> 2;
+        for (int e = lane; e < gpr * hv; e += 64) {
+            const int yy = e / gpr, xx = (e - yy * gpr) << 2;
+            *reinterpret_cast<uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
+                *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
+        }
+    }
+}
+
+}  // namespace p265r

@@ -1,0 +1,476 @@
+// p265r.hip -- host side of the C ABI declared in include/p265r.h.
+//
+// Build (see Makefile):  hipcc --offload-arch=gfx950 -O3 -shared -fPIC -o p265_amd/libp265r.so
+//
+// One context = one HIP device + one non-blocking stream + one parameter set.
+// A batch = one device allocation holding every picture's records, the re-packed
+// coefficient pool, the residual job lists and the output planes.  Run order on the
+// stream: residual kernels (one per job class) -> intra wavefront steps -> SAO.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/p265r.h"
+#include "intra.h"
+#include "residual.h"
+#include "sao.h"
+#include "tables.h"
+
+using namespace p265r;
+
+namespace {
+
+thread_local std::string g_last_hip_error;
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last_hip_error = std::string(what) + ": " + hipGetErrorString(e);
+    return P265R_EHIP;
+}
+
+#define HIP_TRY(expr)                                        \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);    \
+    } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+enum { RC_RAW = RC_NUM, N_POOLS = RC_NUM + 1 };
+
+int tb_class(const p265r_tb& t) {
+    if (t.flags & (P265R_TB_BYPASS | P265R_TB_PCM)) return RC_RAW;
+    if (t.flags & P265R_TB_TSKIP) return RC_TSKIP;
+    switch (t.log2_size) {
+        case 2: return t.c_idx == 0 ? RC_DST4 : RC_DCT4;
+        case 3: return RC_DCT8;
+        case 4: return RC_DCT16;
+        default: return RC_DCT32;
+    }
+}
+
+bool params_ok(const p265r_params& p) {
+    return p.version == P265R_ABI_VERSION && p.chroma_format_idc == 1 && p.pic_width > 0 && p.pic_height > 0 &&
+           p.pic_width % 8 == 0 && p.pic_height % 8 == 0 && p.ctb_log2_size >= 4 && p.ctb_log2_size <= 6 &&
+           p.min_tb_log2_size >= 2 && p.max_tb_log2_size <= 5 && p.min_tb_log2_size <= p.max_tb_log2_size;
+}
+
+}  // namespace
+
+struct p265r_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    p265r_params params{};
+    Geo geo{};
+    int n_ctus = 0;
+    bool timing = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    p265r_timings last{};
+    bool have_timing = false;
+    p265r_batch* pending = nullptr;
+    std::vector<p265r_picture> pending_pics;
+};
+
+struct p265r_batch {
+    int n_pics = 0;
+    void* mem = nullptr;
+    size_t bytes = 0;
+    DevPic* d_pics = nullptr;
+    int16_t* d_pool = nullptr;
+    int16_t* d_res = nullptr;
+    ResJob* d_jobs[RC_NUM] = {};
+    int n_jobs[RC_NUM] = {};
+    std::vector<DevPic> h_pics;
+    bool sao = false;
+};
+
+namespace {
+
+int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
+    const p265r_params& p = ctx->params;
+    const Geo& g = ctx->geo;
+    if (!pic.ctus || (!pic.tbs && pic.n_tbs) || (!pic.coef && pic.n_coef)) return P265R_EINVAL;
+    const int ctb = 1 << p.ctb_log2_size;
+    for (int rs = 0; rs < ctx->n_ctus; ++rs) {
+        const p265r_ctu& c = pic.ctus[rs];
+        if ((uint64_t)c.tb_begin + c.tb_count > pic.n_tbs) return P265R_ERANGE;
+        for (int k = 0; k < 3; ++k) {
+            if (c.sao_type[k] > 2) return P265R_EINVAL;
+            if (c.sao_type[k] == 2 && c.sao_class[k] > 3) return P265R_EINVAL;
+            if (c.sao_type[k] == 1 && c.sao_class[k] > 31) return P265R_EINVAL;
+        }
+        const int cx0 = (rs % g.wc) * ctb, cy0 = (rs / g.wc) * ctb;
+        for (uint32_t i = c.tb_begin; i < c.tb_begin + c.tb_count; ++i) {
+            const p265r_tb& t = pic.tbs[i];
+            if (t.log2_size < 2 || t.log2_size > 5 || t.c_idx > 2 || t.pred_mode > 34) return P265R_EINVAL;
+            const int sub = t.c_idx ? 1 : 0;
+            const int n = 1 << t.log2_size;
+            const int xl = t.x << sub, yl = t.y << sub, nl = n << sub;
+            if (xl + nl > p.pic_width || yl + nl > p.pic_height) return P265R_ERANGE;
+            if (xl < cx0 || yl < cy0 || xl + nl > cx0 + ctb || yl + nl > cy0 + ctb) return P265R_ERANGE;
+            if ((t.x & 3) || (t.y & 3) || (t.x & (n - 1)) || (t.y & (n - 1))) return P265R_EINVAL;
+            if (t.flags & (P265R_TB_CBF | P265R_TB_PCM)) {
+                if ((uint64_t)t.coef_off + (uint64_t)n * n > pic.n_coef) return P265R_ERANGE;
+            }
+            if (t.flags & ~0x0fu) return P265R_EINVAL;
+        }
+    }
+    return P265R_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t p265r_abi_version(void) { return P265R_ABI_VERSION; }
+
+const char* p265r_last_hip_error(void) { return g_last_hip_error.c_str(); }
+
+const char* p265r_strerror(int code) {
+    switch (code) {
+        case P265R_OK: return "ok";
+        case P265R_EINVAL: return "invalid argument or malformed record";
+        case P265R_ENOMEM: return "out of memory";
+        case P265R_EHIP: return "HIP runtime error";
+        case P265R_EUNSUPPORTED: return "unsupported stream feature";
+        case P265R_ERANGE: return "record points outside the picture or its buffers";
+        case P265R_ESTATE: return "call out of order";
+        case P265R_ENODEV: return "no such HIP device";
+        default: return "unknown error";
+    }
+}
+
+int p265r_device_count(void) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) return 0;
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    return n;
+}
+
+int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
+    if (!params || !out) return P265R_EINVAL;
+    *out = nullptr;
+    const p265r_params& p = *params;
+    if (!params_ok(p)) return P265R_EINVAL;
+    if (p.bit_depth_luma != 8 || p.bit_depth_chroma != 8 || p.scaling_list_enabled) return P265R_EUNSUPPORTED;
+    const int n = p265r_device_count();
+    if (n < 0) return n;
+    if (device < 0 || device >= n) return P265R_ENODEV;
+    p265r_ctx* ctx = new (std::nothrow) p265r_ctx();
+    if (!ctx) return P265R_ENOMEM;
+    ctx->device = device;
+    ctx->params = p;
+    Geo& g = ctx->geo;
+    g.w = p.pic_width; g.h = p.pic_height;
+    g.cw = g.w / 2; g.ch = g.h / 2;
+    g.stride[0] = (int)align_up(g.w, 64);
+    g.stride[1] = g.stride[2] = (int)align_up(g.cw, 64);
+    g.ctb_log2 = p.ctb_log2_size;
+    g.wc = (g.w + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+    g.hc = (g.h + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+    g.bd[0] = p.bit_depth_luma; g.bd[1] = g.bd[2] = p.bit_depth_chroma;
+    g.strong = p.strong_intra_smoothing;
+    g.lf_tiles = p.loop_filter_across_tiles;
+    g.nf_w = (g.w + 7) / 8;
+    ctx->n_ctus = g.wc * g.hc;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+    if (e == hipSuccess) {
+        int8_t ang[35];
+        int16_t inv[35];
+        for (int i = 0; i < 35; ++i) { ang[i] = (int8_t)kIntraPredAngle[i]; inv[i] = (int16_t)kInvAngle[i]; }
+        e = hipMemcpyToSymbol(HIP_SYMBOL(c_angle), ang, sizeof(ang));
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_inv_angle), inv, sizeof(inv));
+    }
+    if (e != hipSuccess) {
+        int rc = hip_fail(e, "p265r_create");
+        p265r_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return P265R_OK;
+}
+
+void p265r_destroy(p265r_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->pending) { (void)hipStreamSynchronize(ctx->stream); p265r_batch_free(ctx, ctx->pending); }
+    for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p265r_batch** out) {
+    if (!ctx || !pics || n_pics <= 0 || !out) return P265R_EINVAL;
+    *out = nullptr;
+    for (int i = 0; i < n_pics; ++i) {
+        int rc = validate_picture(ctx, pics[i]);
+        if (rc) return rc;
+    }
+    const Geo& g = ctx->geo;
+    const int nc = ctx->n_ctus;
+    // ---- pool sizing per class ---------------------------------------------------
+    size_t pool_sz[N_POOLS] = {};
+    size_t n_tbs_total = 0;
+    for (int i = 0; i < n_pics; ++i) {
+        n_tbs_total += pics[i].n_tbs;
+        for (uint32_t t = 0; t < pics[i].n_tbs; ++t) {
+            const p265r_tb& tb = pics[i].tbs[t];
+            if (!(tb.flags & (P265R_TB_CBF | P265R_TB_PCM))) continue;
+            pool_sz[tb_class(tb)] += (size_t)1 << (2 * tb.log2_size);
+        }
+    }
+    size_t pool_base[N_POOLS];
+    size_t pool_total = 0;
+    for (int c = 0; c < N_POOLS; ++c) { pool_base[c] = pool_total; pool_total += pool_sz[c]; }
+    if (pool_total >= (1ull << 32)) return P265R_ERANGE;
+    int n_jobs[RC_NUM] = {};
+    for (int c = 0; c < RC_NUM; ++c) n_jobs[c] = (int)(pool_sz[c] >> (c == RC_DCT8 ? 6 : c == RC_DCT16 ? 8 : c == RC_DCT32 ? 10 : 4));
+    // transform-skip jobs may have any size: count them exactly
+    n_jobs[RC_TSKIP] = 0;
+    for (int i = 0; i < n_pics; ++i)
+        for (uint32_t t = 0; t < pics[i].n_tbs; ++t) {
+            const p265r_tb& tb = pics[i].tbs[t];
+            if ((tb.flags & P265R_TB_CBF) && tb_class(tb) == RC_TSKIP) ++n_jobs[RC_TSKIP];
+        }
+    // ---- device layout -----------------------------------------------------------
+    const bool sao = ctx->params.sample_adaptive_offset != 0;
+    const size_t plane_bytes[3] = {(size_t)g.stride[0] * g.h, (size_t)g.stride[1] * g.ch, (size_t)g.stride[2] * g.ch};
+    const size_t pic_plane_bytes = align_up(plane_bytes[0], 256) + 2 * align_up(plane_bytes[1], 256);
+    size_t off = 0;
+    const size_t o_pics = off; off = align_up(off + sizeof(DevPic) * n_pics, 256);
+    const size_t o_ctus = off; off = align_up(off + sizeof(p265r_ctu) * nc * (size_t)n_pics, 256);
+    const size_t o_tbs = off; off = align_up(off + sizeof(p265r_tb) * n_tbs_total, 256);
+    const size_t o_pool = off; off = align_up(off + sizeof(int16_t) * pool_total, 256);
+    const size_t o_res = off; off = align_up(off + sizeof(int16_t) * pool_total, 256);
+    size_t o_jobs[RC_NUM];
+    for (int c = 0; c < RC_NUM; ++c) { o_jobs[c] = off; off = align_up(off + sizeof(ResJob) * n_jobs[c], 256); }
+    size_t o_nf = off;
+    size_t nf_bytes = (size_t)g.nf_w * ((g.h + 7) / 8);
+    size_t n_nf = 0;
+    for (int i = 0; i < n_pics; ++i) n_nf += pics[i].nofilter ? 1 : 0;
+    off = align_up(off + nf_bytes * n_nf, 256);
+    const size_t o_rec = off; off += pic_plane_bytes * n_pics;
+    const size_t o_out = off; if (sao) off += pic_plane_bytes * n_pics;
+    const size_t total = align_up(off, 256);
+
+    // ---- host staging ------------------------------------------------------------
+    std::vector<unsigned char> host;
+    try { host.resize(o_rec); } catch (...) { return P265R_ENOMEM; }
+    p265r_batch* b = new (std::nothrow) p265r_batch();
+    if (!b) return P265R_ENOMEM;
+    (void)hipSetDevice(ctx->device);
+    hipError_t e = hipMalloc(&b->mem, total);
+    if (e != hipSuccess) { delete b; return e == hipErrorOutOfMemory ? P265R_ENOMEM : hip_fail(e, "hipMalloc"); }
+    b->bytes = total;
+    b->n_pics = n_pics;
+    b->sao = sao;
+    unsigned char* dbase = static_cast<unsigned char*>(b->mem);
+    b->d_pics = reinterpret_cast<DevPic*>(dbase + o_pics);
+    b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
+    b->d_res = reinterpret_cast<int16_t*>(dbase + o_res);
+    for (int c = 0; c < RC_NUM; ++c) { b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]); b->n_jobs[c] = n_jobs[c]; }
+    b->h_pics.resize(n_pics);
+
+    p265r_ctu* h_ctus = reinterpret_cast<p265r_ctu*>(host.data() + o_ctus);
+    p265r_tb* h_tbs = reinterpret_cast<p265r_tb*>(host.data() + o_tbs);
+    int16_t* h_pool = reinterpret_cast<int16_t*>(host.data() + o_pool);
+    ResJob* h_jobs[RC_NUM];
+    for (int c = 0; c < RC_NUM; ++c) h_jobs[c] = reinterpret_cast<ResJob*>(host.data() + o_jobs[c]);
+    size_t pool_fill[N_POOLS];
+    std::copy(pool_base, pool_base + N_POOLS, pool_fill);
+    int job_fill[RC_NUM] = {};
+    size_t tb_fill = 0, nf_fill = 0;
+    for (int i = 0; i < n_pics; ++i) {
+        const p265r_picture& pic = pics[i];
+        std::memcpy(h_ctus + (size_t)i * nc, pic.ctus, sizeof(p265r_ctu) * nc);
+        p265r_tb* tb_dst = h_tbs + tb_fill;
+        for (uint32_t t = 0; t < pic.n_tbs; ++t) {
+            p265r_tb tb = pic.tbs[t];
+            if (tb.flags & (P265R_TB_CBF | P265R_TB_PCM)) {
+                const int cls = tb_class(tb);
+                const size_t nn = (size_t)1 << (2 * tb.log2_size);
+                std::memcpy(h_pool + pool_fill[cls], pic.coef + tb.coef_off, nn * sizeof(int16_t));
+                tb.coef_off = (uint32_t)pool_fill[cls];
+                if (cls < RC_NUM) h_jobs[cls][job_fill[cls]++] = ResJob{tb.coef_off, tb.qp, tb.flags, tb.log2_size, tb.c_idx};
+                pool_fill[cls] += nn;
+            }
+            tb_dst[t] = tb;
+        }
+        DevPic& dp = b->h_pics[i];
+        dp.ctus = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus) + (size_t)i * nc;
+        dp.tbs = reinterpret_cast<const p265r_tb*>(dbase + o_tbs) + tb_fill;
+        unsigned char* rec = dbase + o_rec + pic_plane_bytes * i;
+        dp.rec[0] = rec;
+        dp.rec[1] = rec + align_up(plane_bytes[0], 256);
+        dp.rec[2] = dp.rec[1] + align_up(plane_bytes[1], 256);
+        if (sao) {
+            unsigned char* o = dbase + o_out + pic_plane_bytes * i;
+            dp.out[0] = o;
+            dp.out[1] = o + align_up(plane_bytes[0], 256);
+            dp.out[2] = dp.out[1] + align_up(plane_bytes[1], 256);
+        } else {
+            for (int c = 0; c < 3; ++c) dp.out[c] = dp.rec[c];
+        }
+        if (pic.nofilter) {
+            std::memcpy(host.data() + o_nf + nf_fill * nf_bytes, pic.nofilter, nf_bytes);
+            dp.nofilter = dbase + o_nf + nf_fill * nf_bytes;
+            ++nf_fill;
+        } else {
+            dp.nofilter = nullptr;
+        }
+        tb_fill += pic.n_tbs;
+    }
+    std::memcpy(host.data() + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
+    e = hipMemcpy(b->mem, host.data(), o_rec, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { int rc = hip_fail(e, "hipMemcpy(upload)"); (void)hipFree(b->mem); delete b; return rc; }
+    *out = b;
+    return P265R_OK;
+}
+
+int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
+    if (!ctx || !b) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const Geo& g = ctx->geo;
+    p265r_timings tm{};
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    // ---- residual phase ----------------------------------------------------------
+    const int bdl = g.bd[0], bdc = g.bd[1];
+    if (b->n_jobs[RC_DST4]) {
+        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl);
+        ++tm.residual_launches;
+    }
+    if (b->n_jobs[RC_DCT4]) {
+        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc);
+        ++tm.residual_launches;
+    }
+    if (b->n_jobs[RC_DCT8]) {
+        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc);
+        ++tm.residual_launches;
+    }
+    if (b->n_jobs[RC_DCT16]) {
+        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc);
+        ++tm.residual_launches;
+    }
+    if (b->n_jobs[RC_DCT32]) {
+        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc);
+        ++tm.residual_launches;
+    }
+    if (b->n_jobs[RC_TSKIP]) {
+        residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
+        ++tm.residual_launches;
+    }
+    HIP_TRY(hipGetLastError());
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    // ---- intra wavefront: one launch per anti-diagonal s = cx + 2*cy ----------------
+    const int n_steps = (g.wc - 1) + 2 * (g.hc - 1) + 1;
+    for (int step = 0; step < n_steps; ++step) {
+        const int d = step - (g.wc - 1);
+        const int cy_min = d > 0 ? (d + 1) / 2 : 0;
+        const int cy_max = std::min(g.hc - 1, step / 2);
+        if (cy_max < cy_min) continue;
+        dim3 grid(cy_max - cy_min + 1, b->n_pics);
+        intra_step_kernel<<<grid, 64, 0, s>>>(b->d_pics, b->d_pool, b->d_res, g, step, cy_min);
+        ++tm.intra_launches;
+    }
+    HIP_TRY(hipGetLastError());
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    // ---- SAO -----------------------------------------------------------------------
+    if (b->sao) {
+        sao_kernel<<<dim3(ctx->n_ctus, b->n_pics), 256, 0, s>>>(b->d_pics, g);
+        ++tm.sao_launches;
+        HIP_TRY(hipGetLastError());
+    }
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[3], s));
+    ctx->last = tm;
+    ctx->have_timing = ctx->timing;
+    return P265R_OK;
+}
+
+int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pics, int n_pics) {
+    if (!ctx || !b || !pics || n_pics != b->n_pics) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const Geo& g = ctx->geo;
+    const int wd[3] = {g.w, g.cw, g.cw}, ht[3] = {g.h, g.ch, g.ch};
+    for (int i = 0; i < n_pics; ++i)
+        for (int c = 0; c < 3; ++c) {
+            if (pics[i].out[c])
+                HIP_TRY(hipMemcpy2DAsync(pics[i].out[c], wd[c], b->h_pics[i].out[c], g.stride[c], wd[c], ht[c],
+                                         hipMemcpyDeviceToHost, ctx->stream));
+            if (pics[i].recon[c])
+                HIP_TRY(hipMemcpy2DAsync(pics[i].recon[c], wd[c], b->h_pics[i].rec[c], g.stride[c], wd[c], ht[c],
+                                         hipMemcpyDeviceToHost, ctx->stream));
+        }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return P265R_OK;
+}
+
+int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
+    if (!ctx || !b) return P265R_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->pending == b) ctx->pending = nullptr;
+    hipError_t e = b->mem ? hipFree(b->mem) : hipSuccess;
+    delete b;
+    return e == hipSuccess ? P265R_OK : hip_fail(e, "hipFree");
+}
+
+int p265r_submit(p265r_ctx* ctx, const p265r_picture* pics, int n_pics) {
+    if (!ctx) return P265R_EINVAL;
+    if (ctx->pending) return P265R_ESTATE;
+    p265r_batch* b = nullptr;
+    int rc = p265r_batch_upload(ctx, pics, n_pics, &b);
+    if (rc) return rc;
+    rc = p265r_batch_run(ctx, b);
+    if (rc) { p265r_batch_free(ctx, b); return rc; }
+    ctx->pending = b;
+    ctx->pending_pics.assign(pics, pics + n_pics);
+    return P265R_OK;
+}
+
+int p265r_wait(p265r_ctx* ctx) {
+    if (!ctx) return P265R_EINVAL;
+    if (!ctx->pending) return P265R_ESTATE;
+    p265r_batch* b = ctx->pending;
+    int rc = p265r_batch_download(ctx, b, ctx->pending_pics.data(), (int)ctx->pending_pics.size());
+    ctx->pending = nullptr;
+    ctx->pending_pics.clear();
+    int rc2 = p265r_batch_free(ctx, b);
+    return rc ? rc : rc2;
+}
+
+int p265r_sync(p265r_ctx* ctx) {
+    if (!ctx) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return P265R_OK;
+}
+
+int p265r_set_timing(p265r_ctx* ctx, int enable) {
+    if (!ctx) return P265R_EINVAL;
+    ctx->timing = enable != 0;
+    return P265R_OK;
+}
+
+int p265r_last_timings(p265r_ctx* ctx, p265r_timings* out) {
+    if (!ctx || !out) return P265R_EINVAL;
+    if (!ctx->have_timing) return P265R_ESTATE;
+    HIP_TRY(hipEventSynchronize(ctx->ev[3]));
+    float a = 0, b = 0, c = 0, t = 0;
+    HIP_TRY(hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]));
+    HIP_TRY(hipEventElapsedTime(&c, ctx->ev[2], ctx->ev[3]));
+    HIP_TRY(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[3]));
+    p265r_timings r = ctx->last;
+    r.residual_ms = a; r.intra_ms = b; r.sao_ms = c; r.total_ms = t;
+    *out = r;
+    return P265R_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,215 @@
+// Residual phase: scaling (8.6.3) + inverse DCT/DST (8.6.4.2) + bdShift (8.6.2).
+//
+// Replaces decoder/scaling.py:4-47 and decoder/transform.py:74-109 (the reference's
+// 1-D inverse indexes the matrix transposed and samples the wrong axis; this follows
+// the spec, checked against oracle/recon_oracle.py:residual_block).
+//
+// Data layout: the batch's coefficients are re-packed at upload into one int16 pool,
+// grouped by job class (luma 4x4 DST, chroma 4x4 DCT, 8x8, 16x16, 32x32, transform
+// skip), each TB's N*N levels contiguous in raster [y][x] order.  Each kernel streams
+// its class's slab and writes residual samples r[y][x] at the same offsets of a
+// separate int16 buffer (clamped to int16, exact for BitDepth <= 15 because the
+// reconstruction clips), so a resident batch can be re-run.
+// HBM traffic per coefficient: 2 B read + 2 B write; no MFMA (integer butterflies).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "tables.h"
+
+namespace p265r {
+
+struct ResJob {          // 8 bytes, one per coded TB, in pool order within its class
+    uint32_t off;        // int16 offset of the TB in the pool
+    uint8_t  qp;         // qP (incl. QpBdOffset)
+    uint8_t  flags;      // P265R_TB_*
+    uint8_t  log2;
+    uint8_t  c_idx;
+};
+
+enum ResClass { RC_DST4 = 0, RC_DCT4, RC_DCT8, RC_DCT16, RC_DCT32, RC_TSKIP, RC_NUM };
+
+__device__ __forceinline__ int clamp16(long long v) {
+    return v < -32768 ? -32768 : (v > 32767 ? 32767 : (int)v);
+}
+__device__ __forceinline__ int clamp16i(int v) {
+    return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
+}
+
+// d = Clip3(-32768, 32767, (L * 16 * levelScale[qP%6] << (qP/6) + (1 << (bdShift-1))) >> bdShift)
+// computed exactly in 32 bits: |L*16*72| < 2^31, and the shift pair is folded.
+struct Dequant {
+    int scale, lshift, rshift, rnd;
+    __device__ __forceinline__ Dequant(int qp, int bd_shift) {
+        const int per = qp / 6;
+        scale = 16 * (qp % 6 == 0 ? 40 : qp % 6 == 1 ? 45 : qp % 6 == 2 ? 51 : qp % 6 == 3 ? 57 : qp % 6 == 4 ? 64 : 72);
+        if (per >= bd_shift) { lshift = per - bd_shift; rshift = 0; rnd = 0; }
+        else { lshift = 0; rshift = bd_shift - per; rnd = 1 << (rshift - 1); }
+    }
+    __device__ __forceinline__ int operator()(int level) const {
+        long long p = (long long)(level * scale);
+        return clamp16(((p << lshift) + rnd) >> rshift);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// 4x4: one thread per TB, everything in registers.
+// ---------------------------------------------------------------------------
+template <bool DST>
+__device__ __forceinline__ int t4(int j, int i) { return DST ? kDST4[j][i] : kDCT32[j * 8][i]; }
+
+template <bool DST>
+__global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restrict__ pool,
+                                                        int16_t* __restrict__ res,
+                                                        const ResJob* __restrict__ jobs, int n_jobs,
+                                                        int bit_depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_jobs) return;
+    const ResJob jb = jobs[i];
+    const int16_t* blk = pool + jb.off;
+    int16_t* dst = res + jb.off;
+    const uint4 raw0 = *reinterpret_cast<const uint4*>(blk);       // 16 x int16 = 32 B
+    const uint4 raw1 = *reinterpret_cast<const uint4*>(blk + 8);
+    const uint32_t w[8] = {raw0.x, raw0.y, raw0.z, raw0.w, raw1.x, raw1.y, raw1.z, raw1.w};
+    const Dequant dq(jb.qp, bit_depth + 2 - 5);
+    int d[4][4];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int lv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffff);
+        d[k >> 2][k & 3] = dq(lv);
+    }
+    int g[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {            // columns: e[y][x] = sum_j T[j][y] d[j][x]
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            int e = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e += t4<DST>(j, y) * d[j][x];
+            g[y][x] = clamp16i((e + 64) >> 7);
+        }
+    }
+    const int bd2 = 20 - bit_depth;
+    const int rnd2 = 1 << (bd2 - 1);
+    uint32_t o[8];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        int r[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            int acc = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc += t4<DST>(j, x) * g[y][j];
+            r[x] = clamp16i((acc + rnd2) >> bd2);
+        }
+        o[y * 2 + 0] = (uint32_t)(uint16_t)r[0] | ((uint32_t)(uint16_t)r[1] << 16);
+        o[y * 2 + 1] = (uint32_t)(uint16_t)r[2] | ((uint32_t)(uint16_t)r[3] << 16);
+    }
+    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<uint4*>(dst + 8) = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// ---------------------------------------------------------------------------
+// NxN, N = 8/16/32: N threads per TB (256/N TBs per 256-thread block).
+//   load row r (16-B vectors) -> dequant -> LDS [r][c]
+//   thread c: column transform (stage 1) + (e+64)>>7 clip -> LDS [k][c]
+//   thread r: row transform (stage 2) + bdShift -> 16-B vector stores, in place.
+// Matrix entries are compile-time immediates (fully unrolled).
+// ---------------------------------------------------------------------------
+template <int LOG2>
+__global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restrict__ pool,
+                                                       int16_t* __restrict__ res,
+                                                       const ResJob* __restrict__ jobs, int n_jobs,
+                                                       int bit_depth_luma, int bit_depth_chroma) {
+    constexpr int N = 1 << LOG2;
+    constexpr int TPB = 256 / N;                 // TBs per block
+    constexpr int S = N + 2;                     // padded LDS row (odd dword stride)
+    constexpr int STEP = 32 / N;
+    __shared__ int16_t tile[TPB][N * S];
+    const int local = threadIdx.x / N;
+    const int lane = threadIdx.x % N;            // row index (load/store) and column index (stage 1)
+    const int job = blockIdx.x * TPB + local;
+    const bool active = job < n_jobs;
+    int16_t* t = tile[local];
+    ResJob jb = active ? jobs[job] : ResJob{0, 0, 0, 0, 0};
+    const int16_t* blk = pool + jb.off;
+    int16_t* dst = res + jb.off;
+    const int bit_depth = jb.c_idx ? bit_depth_chroma : bit_depth_luma;
+    if (active) {
+        const Dequant dq(jb.qp, bit_depth + LOG2 - 5);
+#pragma unroll
+        for (int v = 0; v < N / 8; ++v) {
+            const uint4 raw = *reinterpret_cast<const uint4*>(blk + lane * N + v * 8);
+            const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int lv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffff);
+                t[lane * S + v * 8 + k] = (int16_t)dq(lv);
+            }
+        }
+    }
+    __syncthreads();
+    if (active) {
+        int col[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) col[k] = t[k * S + lane];
+#pragma unroll
+        for (int y = 0; y < N; ++y) {
+            int e = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) e += kDCT32[k * STEP][y] * col[k];
+            t[y * S + lane] = (int16_t)clamp16i((e + 64) >> 7);
+        }
+    }
+    __syncthreads();
+    if (active) {
+        int row[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) row[k] = t[lane * S + k];
+        const int bd2 = 20 - bit_depth;
+        const int rnd2 = 1 << (bd2 - 1);
+#pragma unroll
+        for (int v = 0; v < N / 8; ++v) {
+            uint32_t o[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                int r2[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int x = v * 8 + h * 2 + q;
+                    int acc = 0;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) acc += kDCT32[k * STEP][x] * row[k];
+                    r2[q] = clamp16i((acc + rnd2) >> bd2);
+                }
+                o[h] = (uint32_t)(uint16_t)r2[0] | ((uint32_t)(uint16_t)r2[1] << 16);
+            }
+            *reinterpret_cast<uint4*>(dst + lane * N + v * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Transform skip (any size): r = (d << tsShift + rnd) >> bdShift, tsShift = 5 + log2.
+// One thread per TB (rare: ~0.8 % of luma 4x4 in the sanity.bin mix).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void residual_tskip_kernel(const int16_t* __restrict__ pool,
+                                                             int16_t* __restrict__ res,
+                                                             const ResJob* __restrict__ jobs, int n_jobs,
+                                                             int bit_depth_luma, int bit_depth_chroma) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_jobs) return;
+    const ResJob jb = jobs[i];
+    const int bd = jb.c_idx ? bit_depth_chroma : bit_depth_luma;
+    const Dequant dq(jb.qp, bd + jb.log2 - 5);
+    const int ts = 5 + jb.log2;
+    const int bd2 = 20 - bd;
+    const int n2 = 1 << (2 * jb.log2);
+    const int16_t* blk = pool + jb.off;
+    int16_t* dst = res + jb.off;
+    for (int k = 0; k < n2; ++k) {
+        const long long r = (long long)dq(blk[k]) << ts;
+        dst[k] = (int16_t)clamp16((r + (1 << (bd2 - 1))) >> bd2);
+    }
+}
+
+}  // namespace p265r

@@ -1,0 +1,158 @@
+"""Host API of the MI355X reconstruction back-end (Python side of the C ABI).
+
+Mirrors what the reference's reconstruction hook would do per picture
+(decoder/cu.py:483-494 -> decode_intra, decoder/sao.py), but per batch:
+
+    ctx = ReconContext(params, device=0)
+    frames = ctx.decode([pic0, pic1, ...])          # -> [(Y, Cb, Cr), ...] uint8 planes
+
+or, keeping inputs resident in HBM (the benchmark path):
+
+    batch = ctx.upload(pics); ctx.run(batch); ctx.sync(); frames = ctx.download(batch)
+
+Errors raise ``P265RError`` (negative C return codes); there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import records as R
+
+
+def _params_c(p):
+    c = _lib.Params()
+    for name, _ in _lib.Params._fields_:
+        if name == "reserved":
+            continue
+        setattr(c, name, int(p[name]))
+    return c
+
+
+def plane_shapes(params):
+    w, h = int(params["pic_width"]), int(params["pic_height"])
+    return [(h, w), (h // 2, w // 2), (h // 2, w // 2)]
+
+
+class Batch:
+    def __init__(self, ctx, handle, pics, keep):
+        self.ctx, self.handle, self.pics, self._keep = ctx, handle, pics, keep
+
+    def free(self):
+        if self.handle:
+            _lib.check(self.ctx.lib.p265r_batch_free(self.ctx.handle, self.handle), "p265r_batch_free")
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class ReconContext:
+    """One HIP device + stream + parameter set (p265r_ctx)."""
+
+    def __init__(self, params, device=0):
+        self.lib = _lib.load()
+        self.params = params
+        self._pc = _params_c(params)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.p265r_create(device, ctypes.byref(self._pc), ctypes.byref(h)), "p265r_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.p265r_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- marshalling ------------------------------------------------------------
+    def _pictures_c(self, pics, outs=None, recons=None):
+        keep = []
+        arr = (_lib.PictureC * len(pics))()
+        for i, p in enumerate(pics):
+            R.validate(self.params, p)
+            ctus = np.ascontiguousarray(p.ctus, R.CTU_DTYPE)
+            tbs = np.ascontiguousarray(p.tbs, R.TB_DTYPE)
+            coef = np.ascontiguousarray(p.coef, np.int16)
+            keep += [ctus, tbs, coef]
+            c = arr[i]
+            c.ctus = ctus.ctypes.data
+            c.tbs = tbs.ctypes.data if len(tbs) else None
+            c.n_tbs = len(tbs)
+            c.coef = coef.ctypes.data if len(coef) else None
+            c.n_coef = len(coef)
+            if p.nofilter is not None:
+                nf = np.ascontiguousarray(p.nofilter, np.uint8)
+                keep.append(nf)
+                c.nofilter = nf.ctypes.data
+            for k in range(3):
+                if outs is not None:
+                    c.out[k] = outs[i][k].ctypes.data
+                if recons is not None:
+                    c.recon[k] = recons[i][k].ctypes.data
+        return arr, keep
+
+    def _alloc_planes(self, n):
+        return [[np.empty(s, np.uint8) for s in plane_shapes(self.params)] for _ in range(n)]
+
+    # ---- batch API --------------------------------------------------------------
+    def upload(self, pics):
+        arr, keep = self._pictures_c(pics)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.p265r_batch_upload(self.handle, arr, len(pics), ctypes.byref(h)), "p265r_batch_upload")
+        return Batch(self, h, pics, keep)
+
+    def run(self, batch):
+        _lib.check(self.lib.p265r_batch_run(self.handle, batch.handle), "p265r_batch_run")
+
+    def download(self, batch, with_recon=False):
+        outs = self._alloc_planes(len(batch.pics))
+        recs = self._alloc_planes(len(batch.pics)) if with_recon else None
+        arr = (_lib.PictureC * len(batch.pics))()
+        for i in range(len(batch.pics)):
+            for k in range(3):
+                arr[i].out[k] = outs[i][k].ctypes.data
+                if recs is not None:
+                    arr[i].recon[k] = recs[i][k].ctypes.data
+        _lib.check(self.lib.p265r_batch_download(self.handle, batch.handle, arr, len(batch.pics)),
+                   "p265r_batch_download")
+        return (outs, recs) if with_recon else outs
+
+    def sync(self):
+        _lib.check(self.lib.p265r_sync(self.handle), "p265r_sync")
+
+    def set_timing(self, on=True):
+        _lib.check(self.lib.p265r_set_timing(self.handle, int(bool(on))), "p265r_set_timing")
+
+    def last_timings(self):
+        t = _lib.Timings()
+        _lib.check(self.lib.p265r_last_timings(self.handle, ctypes.byref(t)), "p265r_last_timings")
+        return {f: getattr(t, f) for f, _ in _lib.Timings._fields_ if f != "reserved"}
+
+    # ---- one-shot API (submit / wait) -------------------------------------------------
+    def decode(self, pics, with_recon=False):
+        outs = self._alloc_planes(len(pics))
+        recs = self._alloc_planes(len(pics)) if with_recon else None
+        arr, keep = self._pictures_c(pics, outs, recs)
+        _lib.check(self.lib.p265r_submit(self.handle, arr, len(pics)), "p265r_submit")
+        _lib.check(self.lib.p265r_wait(self.handle), "p265r_wait")
+        del keep
+        return (outs, recs) if with_recon else outs
+
+
+def device_count():
+    return _lib.check(_lib.load().p265r_device_count(), "p265r_device_count")

@@ -1,0 +1,138 @@
+"""Record format of the reconstruction batch (numpy mirror of include/p265r.h).
+
+The reference decoder keeps everything the hot path needs inside its syntax-tree
+objects (decoder/cu.py, decoder/tu.py, decoder/sao.py) and reads it back per sample
+through tree walks (tu.py:667-701, ctu.py:33-71).  The MI355X back-end instead
+receives flat, fixed-size records per picture:
+
+  CTU_DTYPE  one per CTU (raster order): TB range, slice/tile ids, SAO parameters
+  TB_DTYPE   one per transform block in decode order: position, size, component,
+             intra mode, flags, qP, offset of its dense int16 coefficients
+  coef       int16 TransCoeffLevel, N*N raster [y][x] per coded TB
+
+``Picture`` bundles them; ``Params`` is the 32-byte sequence-parameter POD.
+"""
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+ABI_VERSION = 1
+
+TB_CBF, TB_TSKIP, TB_BYPASS, TB_PCM = 0x01, 0x02, 0x04, 0x08
+CTU_LF_ACROSS_SLICES = 0x01
+
+PARAMS_DTYPE = np.dtype([
+    ("version", "<u4"), ("pic_width", "<u2"), ("pic_height", "<u2"),
+    ("chroma_format_idc", "u1"), ("bit_depth_luma", "u1"), ("bit_depth_chroma", "u1"),
+    ("ctb_log2_size", "u1"), ("min_tb_log2_size", "u1"), ("max_tb_log2_size", "u1"),
+    ("strong_intra_smoothing", "u1"), ("constrained_intra_pred", "u1"),
+    ("sample_adaptive_offset", "u1"), ("loop_filter_across_tiles", "u1"),
+    ("scaling_list_enabled", "u1"), ("reserved", "u1", 13)])
+assert PARAMS_DTYPE.itemsize == 32
+
+CTU_DTYPE = np.dtype([
+    ("tb_begin", "<u4"), ("tb_count", "<u2"), ("tile_id", "<u2"), ("slice_addr", "<u4"),
+    ("flags", "u1"), ("sao_type", "u1", 3), ("sao_class", "u1", 3), ("reserved", "u1"),
+    ("sao_offset", "i1", (3, 4))])
+assert CTU_DTYPE.itemsize == 32
+
+TB_DTYPE = np.dtype([
+    ("x", "<u2"), ("y", "<u2"), ("log2_size", "u1"), ("c_idx", "u1"), ("pred_mode", "u1"),
+    ("flags", "u1"), ("qp", "u1"), ("reserved", "u1", 3), ("coef_off", "<u4")])
+assert TB_DTYPE.itemsize == 16
+
+PARAM_KEYS = [n for n in PARAMS_DTYPE.names if n not in ("version", "reserved")]
+
+
+def make_params(**kw) -> np.ndarray:
+    """Build a params record; unspecified fields default to the sanity.bin-like SPS/PPS."""
+    d = dict(pic_width=352, pic_height=288, chroma_format_idc=1, bit_depth_luma=8,
+             bit_depth_chroma=8, ctb_log2_size=6, min_tb_log2_size=2, max_tb_log2_size=5,
+             strong_intra_smoothing=1, constrained_intra_pred=0, sample_adaptive_offset=1,
+             loop_filter_across_tiles=1, scaling_list_enabled=0)
+    for k, v in kw.items():
+        if k not in d:
+            raise KeyError("unknown params field %r" % k)
+        d[k] = v
+    p = np.zeros((), PARAMS_DTYPE)
+    p["version"] = ABI_VERSION
+    for k, v in d.items():
+        p[k] = v
+    return p
+
+
+def params_dict(p) -> dict:
+    return {k: int(p[k]) for k in PARAM_KEYS}
+
+
+def ctb_grid(p):
+    ctb = 1 << int(p["ctb_log2_size"])
+    w, h = int(p["pic_width"]), int(p["pic_height"])
+    return (w + ctb - 1) // ctb, (h + ctb - 1) // ctb
+
+
+@dataclass
+class Picture:
+    """Records of one picture (the C struct p265r_picture without the output planes)."""
+    ctus: np.ndarray                      # CTU_DTYPE, raster order
+    tbs: np.ndarray                       # TB_DTYPE
+    coef: np.ndarray                      # int16
+    nofilter: Optional[np.ndarray] = None  # uint8 per 8x8 luma block or None
+    meta: dict = field(default_factory=dict)
+
+    def as_oracle_dict(self):
+        return {"ctus": self.ctus, "tbs": self.tbs, "coef": self.coef, "nofilter": self.nofilter}
+
+    @property
+    def n_coded_coef(self):
+        m = (self.tbs["flags"] & (TB_CBF | TB_PCM)) != 0
+        return int(np.sum(1 << (2 * self.tbs["log2_size"][m].astype(np.int64))))
+
+
+class RecordError(ValueError):
+    pass
+
+
+def validate(params, pic: Picture):
+    """Host-side checks mirroring the C++ ones (p265_amd/csrc/p265r.hip: validate_picture).
+
+    The kernels assume every record lies inside its CTU and picture; these checks are
+    what keeps a malformed record from faulting the GPU.
+    """
+    wc, hc = ctb_grid(params)
+    if pic.ctus.dtype != CTU_DTYPE or pic.tbs.dtype != TB_DTYPE or pic.coef.dtype != np.int16:
+        raise RecordError("record dtypes do not match the ABI")
+    if len(pic.ctus) != wc * hc:
+        raise RecordError("expected %d CTUs, got %d" % (wc * hc, len(pic.ctus)))
+    ctb_log2 = int(params["ctb_log2_size"])
+    w, h = int(params["pic_width"]), int(params["pic_height"])
+    tbs = pic.tbs
+    begin = pic.ctus["tb_begin"].astype(np.int64)
+    end = begin + pic.ctus["tb_count"]
+    if (end > len(tbs)).any():
+        raise RecordError("CTU TB range outside the TB array")
+    lg = tbs["log2_size"].astype(np.int64)
+    c = tbs["c_idx"].astype(np.int64)
+    if ((lg < 2) | (lg > 5)).any() or (c > 2).any() or (tbs["pred_mode"] > 34).any():
+        raise RecordError("TB size / component / mode out of range")
+    sub = (c > 0).astype(np.int64)
+    xl, yl = tbs["x"].astype(np.int64) << sub, tbs["y"].astype(np.int64) << sub
+    nl = (1 << lg) << sub
+    if ((xl >= w) | (yl >= h)).any():
+        raise RecordError("TB outside picture")
+    owner = np.repeat(np.arange(len(pic.ctus)), pic.ctus["tb_count"].astype(np.int64))
+    idx = np.concatenate([np.arange(b, e) for b, e in zip(begin, end)]) if len(tbs) else np.zeros(0, np.int64)
+    if len(idx):
+        cx, cy = (owner % wc) << ctb_log2, (owner // wc) << ctb_log2
+        ctb = 1 << ctb_log2
+        bad = ((xl[idx] < cx) | (yl[idx] < cy) | (xl[idx] + nl[idx] > cx + ctb) | (yl[idx] + nl[idx] > cy + ctb))
+        if bad.any():
+            raise RecordError("TB not inside its CTU")
+    coded = (tbs["flags"] & (TB_CBF | TB_PCM)) != 0
+    if (tbs["coef_off"][coded].astype(np.int64) + (1 << (2 * lg[coded])) > len(pic.coef)).any():
+        raise RecordError("coefficient range outside coef array")
+    if (pic.ctus["sao_type"] > 2).any():
+        raise RecordError("bad SaoTypeIdx")
+    if pic.nofilter is not None and len(pic.nofilter) != ((w + 7) // 8) * ((h + 7) // 8):
+        raise RecordError("nofilter map has the wrong size")
