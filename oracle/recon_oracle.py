@@ -321,7 +321,7 @@ def _recon_tb(geo, planes, t, coef, bd, strong):
     flags, mode = int(t["flags"]), int(t["pred_mode"])
     plane = planes[c_idx]
     sub = 0 if c_idx == 0 else 1
-    if flags & TB_CBF:
+    if flags & (TB_CBF | TB_PCM):
         off = int(t["coef_off"])
         level = np.asarray(coef[off: off + n * n], np.int64).reshape(n, n)
         res = residual_block(level, log2, c_idx, int(t["qp"]), flags, bd[c_idx])
