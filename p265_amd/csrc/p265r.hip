@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -17,6 +18,7 @@
 
 #include "../../include/p265r.h"
 #include "intra.h"
+#include "intra_rows.h"
 #include "residual.h"
 #include "sao.h"
 #include "tables.h"
@@ -73,6 +75,9 @@ struct p265r_ctx {
     bool have_timing = false;
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
+    int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
+    int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16)
+    int num_cus = 256;
 };
 
 struct p265r_batch {
@@ -82,6 +87,7 @@ struct p265r_batch {
     DevPic* d_pics = nullptr;
     int16_t* d_pool = nullptr;
     int16_t* d_res = nullptr;
+    int* d_err = nullptr;
     ResJob* d_jobs[RC_NUM] = {};
     int n_jobs[RC_NUM] = {};
     std::vector<DevPic> h_pics;
@@ -120,6 +126,31 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
         }
     }
     return P265R_OK;
+}
+
+template <int W>
+int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
+    const Geo& g = ctx->geo;
+    const int fs = (W + g.hc - 1) / g.hc + 1;
+    const size_t lds = 256 + W * sizeof(WaveLds) + (size_t)fs * 2 * (g.w + 2 * g.cw);
+    if (lds > 160 * 1024) return P265R_EUNSUPPORTED;
+    auto fn = intra_rows_kernel<W>;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds));
+    if (per_cu < 1) return P265R_EUNSUPPORTED;
+    const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
+    fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, b->d_err);
+    HIP_TRY(hipGetLastError());
+    return P265R_OK;
+}
+
+int launch_rows(p265r_ctx* ctx, p265r_batch* b) {
+    switch (ctx->row_waves) {
+        case 4: return launch_rows_w<4>(ctx, b);
+        case 16: return launch_rows_w<16>(ctx, b);
+        default: return launch_rows_w<8>(ctx, b);
+    }
 }
 
 }  // namespace
@@ -178,7 +209,13 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.lf_tiles = p.loop_filter_across_tiles;
     g.nf_w = (g.w + 7) / 8;
     ctx->n_ctus = g.wc * g.hc;
+    if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
+    if (const char* v = std::getenv("P265R_ROW_WAVES")) {
+        const int w = std::atoi(v);
+        if (w == 4 || w == 8 || w == 16) ctx->row_waves = w;
+    }
     hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
     if (e == hipSuccess) {
@@ -245,6 +282,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t pic_plane_bytes = align_up(plane_bytes[0], 256) + 2 * align_up(plane_bytes[1], 256);
     size_t off = 0;
     const size_t o_pics = off; off = align_up(off + sizeof(DevPic) * n_pics, 256);
+    const size_t o_err = off; off = align_up(off + 256, 256);
     const size_t o_ctus = off; off = align_up(off + sizeof(p265r_ctu) * nc * (size_t)n_pics, 256);
     const size_t o_tbs = off; off = align_up(off + sizeof(p265r_tb) * n_tbs_total, 256);
     const size_t o_pool = off; off = align_up(off + sizeof(int16_t) * pool_total, 256);
@@ -275,6 +313,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->d_pics = reinterpret_cast<DevPic*>(dbase + o_pics);
     b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
     b->d_res = reinterpret_cast<int16_t*>(dbase + o_res);
+    b->d_err = reinterpret_cast<int*>(dbase + o_err);
     for (int c = 0; c < RC_NUM; ++c) { b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]); b->n_jobs[c] = n_jobs[c]; }
     b->h_pics.resize(n_pics);
 
@@ -369,8 +408,14 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     HIP_TRY(hipGetLastError());
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
-    // ---- intra wavefront: one launch per anti-diagonal s = cx + 2*cy ----------------
-    const int n_steps = (g.wc - 1) + 2 * (g.hc - 1) + 1;
+    // ---- intra wavefront ---------------------------------------------------------------
+    if (ctx->schedule == 1) {
+        HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int), s));
+        int rc = launch_rows(ctx, b);
+        if (rc) return rc;
+        ++tm.intra_launches;
+    }
+    const int n_steps = ctx->schedule == 0 ? (g.wc - 1) + 2 * (g.hc - 1) + 1 : 0;
     for (int step = 0; step < n_steps; ++step) {
         const int d = step - (g.wc - 1);
         const int cy_min = d > 0 ? (d + 1) / 2 : 0;
@@ -409,6 +454,12 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
                                          hipMemcpyDeviceToHost, ctx->stream));
         }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+        g_last_hip_error = "intra row pipeline: dependency wait timed out";
+        return P265R_EHIP;
+    }
     return P265R_OK;
 }
 

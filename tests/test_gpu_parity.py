@@ -41,7 +41,18 @@ def _check(recon_mod, params, pics, label=""):
     return outs
 
 
-def test_sanity_bin_frames(recon_mod):
+@pytest.fixture(params=["rows", "steps", "rows16", "rows4"])
+def schedule(request, monkeypatch):
+    """Both intra schedules (CU-local row pipeline with 4/8/16 waves, per-diagonal launches)."""
+    if request.param == "steps":
+        monkeypatch.setenv("P265R_SCHEDULE", "steps")
+    else:
+        monkeypatch.setenv("P265R_SCHEDULE", "rows")
+        monkeypatch.setenv("P265R_ROW_WAVES", {"rows": "8", "rows16": "16", "rows4": "4"}[request.param])
+    return request.param
+
+
+def test_sanity_bin_frames(recon_mod, schedule):
     params, pics = frontend.pictures_from_frontend_npz(os.path.join(GOLDEN, "sanity_frontend.npz"))
     _check(recon_mod, params, pics, "sanity")
 
@@ -52,13 +63,13 @@ def test_config2_single_ctu(recon_mod):
 
 
 @pytest.mark.parametrize("ctb_log2,w,h", [(6, 352, 288), (5, 200, 136), (4, 72, 40), (6, 136, 72)])
-def test_synthetic_uniform_modes(recon_mod, ctb_log2, w, h):
+def test_synthetic_uniform_modes(recon_mod, schedule, ctb_log2, w, h):
     params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2)
     pics = [synth.make_picture(params, 1000 + 10 * ctb_log2 + s, perf=False) for s in range(3)]
     _check(recon_mod, params, pics, "uniform")
 
 
-def test_slices_tiles_and_loop_filter_flags(recon_mod):
+def test_slices_tiles_and_loop_filter_flags(recon_mod, schedule):
     params = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, loop_filter_across_tiles=0)
     pics = [synth.make_picture(params, 77 + s, perf=False, tiles=(3, 2), n_slices=4, lf_across_slices=None)
             for s in range(3)]
@@ -96,7 +107,7 @@ def test_pcm_blocks(recon_mod):
     _check(recon_mod, params, [b.finish()], "pcm")
 
 
-def test_1080p_frame(recon_mod):
+def test_1080p_frame(recon_mod, schedule):
     params = R.make_params(pic_width=1920, pic_height=1080)
     pics = [synth.make_picture(params, 265 + 3, perf=True)]
     _check(recon_mod, params, pics, "1080p")
@@ -138,3 +149,18 @@ def test_invalid_records_rejected(recon_mod):
     with recon_mod.ReconContext(params) as ctx:
         with pytest.raises(Exception):
             ctx.decode([bad])
+
+
+def test_many_small_pictures_per_workgroup(recon_mod, schedule):
+    """More pictures than resident workgroups: the row queue of one workgroup crosses
+    picture boundaries (several pictures in flight per workgroup, line-buffer slots reused)."""
+    params = R.make_params(pic_width=64, pic_height=128, ctb_log2_size=5)
+    uniq = [synth.make_picture(params, 500 + s, perf=False) for s in range(5)]
+    pics = [uniq[i % 5] for i in range(1200)]
+    with recon_mod.ReconContext(params) as ctx:
+        outs = ctx.decode(pics)
+    pd = R.params_dict(params)
+    refs = [O.decode_picture(pd, u.as_oracle_dict())[1] for u in uniq]
+    for i in range(len(pics)):
+        for c in range(3):
+            np.testing.assert_array_equal(outs[i][c], refs[i % 5][c], err_msg="pic %d c%d" % (i, c))
