@@ -36,8 +36,11 @@ struct WaveLds {                 // one wave's private CTU state (6816 B)
 struct RowCtrl {                 // 256 B at the start of dynamic LDS
     int next_row;
     int error;
-    int prog[62];                // (row & 0xffff) << 16 | CTUs done, ring of 2*W
+    int done[32];                // per picture slot: rows completed (monotonic over generations)
+    int pad[30];
 };
+// Dynamic LDS layout: [RowCtrl 256 B][prog: fs x hc ints][W x WaveLds][fs x 2 line buffers]
+// prog[slot][cy] = (local picture index & 0xffff) << 16 | CTUs done.
 
 __device__ __forceinline__ void wave_sync() {
     // LDS operations of one wavefront execute in program order; only the compiler
@@ -88,12 +91,15 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
     RowCtrl& ctl = *reinterpret_cast<RowCtrl*>(smem);
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    WaveLds& L = reinterpret_cast<WaveLds*>(smem + 256)[wave];
+    const int prog_bytes = (fs_count * g.hc * 4 + 15) & ~15;
+    int* prog = reinterpret_cast<int*>(smem + 256);
+    WaveLds& L = reinterpret_cast<WaveLds*>(smem + 256 + prog_bytes)[wave];
     const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
-    unsigned char* lines = smem + 256 + W * sizeof(WaveLds);
+    unsigned char* lines = smem + 256 + prog_bytes + W * sizeof(WaveLds);
 
     if (threadIdx.x == 0) { ctl.next_row = 0; ctl.error = 0; }
-    if (threadIdx.x < 62) ctl.prog[threadIdx.x] = -1;
+    if (threadIdx.x < 32) ctl.done[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < fs_count * g.hc; i += 64 * W) prog[i] = -1;
     __syncthreads();
 
     const int G = gridDim.x;
@@ -101,7 +107,19 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
     const int n_my = b < n_pics ? (n_pics - b + G - 1) / G : 0;
     const int rows_total = n_my * g.hc;
     const int ctb = 1 << g.ctb_log2;
-    const int ring = 2 * W;
+    // bounded spin-wait on an LDS word; false = gave up (error published, caller returns)
+    auto wait_until = [&](auto ready) -> bool {
+        long spins = 0;
+        for (;;) {
+            if (ready()) return true;
+            if (__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1l << 24)) {                    // never hang the GPU
+                if (lane == 0) { ctl.error = 1; atomicOr(err_flag, 1); }
+                return false;
+            }
+        }
+    };
 
     for (;;) {
         int r = 0;
@@ -109,29 +127,29 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         r = __builtin_amdgcn_readfirstlane(r);
         if (r >= rows_total) break;
         const int j = r / g.hc, cy = r - j * g.hc;
+        const int slot = j % fs_count, gen = j / fs_count;
         const DevPic P = pics[b + j * G];
-        unsigned char* line_cur = lines + (size_t)((j % fs_count) * 2 + (cy & 1)) * line_bytes;
-        const unsigned char* line_up = lines + (size_t)((j % fs_count) * 2 + ((cy & 1) ^ 1)) * line_bytes;
-        int* my_prog = &ctl.prog[r % ring];
-        const int* up_prog = &ctl.prog[(r + ring - 1) % ring];
-        const int tag_up = ((r - 1) & 0xffff) << 16;
-        if (lane == 0) __hip_atomic_store(my_prog, (r & 0xffff) << 16, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // picture slot reuse: every row of picture j waits until picture j - fs_count (the
+        // slot's previous occupant) has completed all its rows; those rows were dequeued
+        // earlier and are held by running waves, so this wait always ends.
+        if (!wait_until([&] {
+                return __hip_atomic_load(&ctl.done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen * g.hc;
+            })) return;
+        unsigned char* line_cur = lines + (size_t)(slot * 2 + (cy & 1)) * line_bytes;
+        const unsigned char* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
+        int* my_prog = &prog[slot * g.hc + cy];
+        const int* up_prog = &prog[slot * g.hc + (cy > 0 ? cy - 1 : 0)];
+        const int tag = (j & 0xffff) << 16;
+        if (lane == 0) __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 
         for (int cx = 0; cx < g.wc; ++cx) {
             // ---- wait for the row above (2-CTU lag) -------------------------------------
             if (cy > 0) {
                 const int need = min(cx + 2, g.wc);
-                long spins = 0;
-                for (;;) {
-                    const int v = __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if ((v & 0xffff0000) == tag_up && (v & 0xffff) >= need) break;
-                    if (__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1l << 24)) {                    // bounded: never hang the GPU
-                        if (lane == 0) { ctl.error = 1; atomicOr(err_flag, 1); }
-                        return;
-                    }
-                }
+                if (!wait_until([&] {
+                        const int v = __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        return (v & 0xffff0000) == tag && (v & 0xffff) >= need;
+                    })) return;
             }
             const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
             const int addr = cy * g.wc + cx;
@@ -377,9 +395,10 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 if (lane < hv) lf[lane] = src[lane * ist + wv - 1];
             }
             if (lane == 0)
-                __hip_atomic_store(my_prog, ((r & 0xffff) << 16) | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             wave_sync();
         }
+        if (lane == 0) __hip_atomic_fetch_add(&ctl.done[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 

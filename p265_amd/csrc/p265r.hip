@@ -131,8 +131,13 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
 template <int W>
 int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
     const Geo& g = ctx->geo;
-    const int fs = (W + g.hc - 1) / g.hc + 1;
-    const size_t lds = 256 + W * sizeof(WaveLds) + (size_t)fs * 2 * (g.w + 2 * g.cw);
+    // picture slots: enough for the W rows in flight to span, plus one of slack
+    int fs = std::min(32, (W + g.hc - 1) / g.hc + 2);
+    auto lds_of = [&](int f) {
+        return 256 + (size_t)((f * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
+    };
+    while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
+    const size_t lds = lds_of(fs);
     if (lds > 160 * 1024) return P265R_EUNSUPPORTED;
     auto fn = intra_rows_kernel<W>;
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
