@@ -83,6 +83,20 @@ __device__ __forceinline__ bool nb_available(int xl, int yl, int xc, int yc, int
     return morton4(xl >> 2, yl >> 2) < morton4(xc >> 2, yc >> 2);
 }
 
+__device__ __forceinline__ bool nb_available_wh(int xl, int yl, int xc, int yc, int x0, int y0,
+                                                int w, int h, int ctb, unsigned flags) {
+    if (x0 + xl >= w || y0 + yl >= h) return false;
+    if (yl < 0) {
+        if (xl < 0) return flags & 4u;
+        if (xl < ctb) return flags & 2u;
+        if (xl < 2 * ctb) return flags & 8u;
+        return false;
+    }
+    if (xl < 0) return (yl < ctb) && (flags & 1u);
+    if (xl >= ctb || yl >= ctb) return false;
+    return morton4(xl >> 2, yl >> 2) < morton4(xc >> 2, yc >> 2);
+}
+
 __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict__ pics,
                                                        const int16_t* __restrict__ pool,
                                                        const int16_t* __restrict__ resid,

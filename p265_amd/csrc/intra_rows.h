@@ -4,14 +4,18 @@
 // (pictures of the workgroup in order, rows top to bottom) and walk each row left to
 // right.  Row r may start CTU cx once row r-1 has finished CTU min(cx+2, wc) - the
 // 2-CTU lag that makes the left, top-left, top and top-right CTUs available.  The
-// queue runs across picture boundaries, so waves never idle at a picture's ramp-down.
+// queue runs across picture boundaries, so waves never idle at a picture's ramp-down;
+// picture slots (line buffers + progress words) are reused only after the slot's
+// previous picture has completed every row.
 //
 // All neighbour data lives in LDS: the row above comes from a per-picture, per-row-
 // parity LINE BUFFER (bottom sample row of every finished CTU), the column on the left
 // is the wave's own previous CTU.  Nothing is re-read from HBM and no cross-CU
 // hand-off exists, so the only synchronisation is one LDS progress word per row
 // (workgroup-scope release/acquire).  Per transform block the wave does three LDS
-// round trips (gather, substitute+filter, predict) with wave-local ordering only.
+// round trips (gather, substitute+filter, predict+reconstruct) with wave-local
+// ordering only; the TB record comes from a VGPR (v_readlane) and its residual was
+// fetched while the previous TB was being processed.
 //
 // Same per-TB arithmetic as intra.h (8.4.4.2.x, 8.6.7); replaces decoder/intra.py:24-305
 // and decoder/reconstruction.py:4-27 driven by decoder/cu.py:595-615.
@@ -24,6 +28,30 @@
 extern "C" __device__ int __ockl_wfred_add_i32(int);
 
 namespace p265r {
+
+#define P265R_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const P265R_GLOBAL T* gptr(const T* p) { return (const P265R_GLOBAL T*)p; }
+template <typename T>
+__device__ __forceinline__ P265R_GLOBAL T* gptr_w(T* p) { return (P265R_GLOBAL T*)p; }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld16(const void* p) {
+    const u32x4_t v = *reinterpret_cast<const P265R_GLOBAL u32x4_t*>(gptr(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// copy a POD struct out of global memory with global (not flat) loads
+template <typename T>
+__device__ __forceinline__ T gload(const T* p) {
+    static_assert(sizeof(T) % 8 == 0, "8-byte granules");
+    const P265R_GLOBAL u32x2_t* q = reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(p));
+    u32x2_t tmp[sizeof(T) / 8];
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 8); ++i) tmp[i] = q[i];
+    T v;
+    __builtin_memcpy(&v, tmp, sizeof(T));
+    return v;
+}
 
 struct WaveLds {                 // one wave's private CTU state (6816 B)
     uint8_t  y[64 * 64];         // interior luma, stride 64
@@ -67,18 +95,186 @@ __device__ __forceinline__ int subst_src(int k, unsigned long long m0, unsigned 
     return -1;
 }
 
-struct TbRec {                    // decoded p265r_tb (wave-uniform)
-    int x, y, log2, c, mode, flags, off;
+struct CtuCtx {                  // wave-uniform state of the CTU being reconstructed
+    int x0, y0, w, h, cw, ctb;
+    unsigned flags;              // bit0 L, bit1 T, bit2 TL, bit3 TR available
+    int bd_l, bd_c, strong;
 };
 
-__device__ __forceinline__ TbRec tb_from_words(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-    TbRec t;
-    t.x = (int)(w0 & 0xffff); t.y = (int)(w0 >> 16);
-    t.log2 = (int)(w1 & 0xff); t.c = (int)((w1 >> 8) & 0xff);
-    t.mode = (int)((w1 >> 16) & 0xff); t.flags = (int)(w1 >> 24);
-    (void)w2;                      // qp (used by the residual phase) + reserved
-    t.off = (int)w3;
-    return t;
+__device__ __forceinline__ int clip_pel(int v, int maxv) { return min(max(v, 0), maxv); }
+
+// Reconstruct one TB of size 2^LOG2.  tw1 = TB record word 1 (log2 | c | mode | flags),
+// (tx, ty) its position; (ra, rb) this lane's residual words (prefetched).
+template <int LOG2>
+__device__ __forceinline__ void recon_tb(const CtuCtx& X, WaveLds& L, const uint8_t* line_up,
+                                        int tx, int ty, int c, int mode, int flags,
+                                        uint4 ra, uint4 rb, int lane) {
+    constexpr int n = 1 << LOG2;
+    constexpr int nn = n * n;
+    constexpr int S = nn >= 64 ? nn / 64 : 1;        // samples per lane (raster run)
+    constexpr int nref = 4 * n + 1;
+    constexpr int NCH = (nref + 63) / 64;
+    const int sub = c ? 1 : 0;
+    const int xr = tx - (X.x0 >> sub), yr = ty - (X.y0 >> sub);
+    const int bd = c ? X.bd_c : X.bd_l;
+    const int maxv = (1 << bd) - 1;
+    uint8_t* interior = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
+    const int ist = c ? 32 : 64;
+    const uint8_t* top = line_up + (c == 0 ? 0 : (c == 1 ? X.w : X.w + X.cw)) + (X.x0 >> sub);
+    const uint8_t* left = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
+    const bool own = lane * S < nn;
+    const int sidx = own ? lane * S : 0;
+    const int sy = sidx >> LOG2, sx = sidx & (n - 1);
+    // (ra, rb): the two aligned 16-B chunks holding this lane's residual run (see res_addr)
+    uint32_t rw[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+    if constexpr (S == 4) {
+        const bool hi = sidx & 4;
+        rw[0] = hi ? ra.z : ra.x; rw[1] = hi ? ra.w : ra.y;
+    } else if constexpr (S == 1) {
+        const int e = sidx & 7;
+        const uint32_t wd = e < 2 ? ra.x : (e < 4 ? ra.y : (e < 6 ? ra.z : ra.w));
+        rw[0] = (e & 1) ? (wd >> 16) : (wd & 0xffffu);
+    }
+    auto resv = [&](int i) { return (int)(int16_t)(rw[i >> 1] >> ((i & 1) * 16)); };
+    uint32_t outw[(S + 3) / 4];
+#pragma unroll
+    for (int q = 0; q < (S + 3) / 4; ++q) outw[q] = 0;
+    auto put = [&](int i, int v) { outw[i >> 2] |= (uint32_t)clip_pel(v + resv(i), maxv) << (8 * (i & 3)); };
+
+    if (flags & P265R_TB_PCM) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) put(i, 0);
+    } else {
+        // ---- A: gather raw reference samples + availability (6.4.1) --------------------
+        const int xcl = xr << sub, ycl = yr << sub;
+        unsigned long long m[3] = {0ull, 0ull, 0ull};
+#pragma unroll
+        for (int jj = 0; jj < NCH; ++jj) {
+            const int k = lane + 64 * jj;
+            bool av = false;
+            if (k < nref) {
+                const int dx = k <= 2 * n ? -1 : k - 2 * n - 1;
+                const int dy = k < 2 * n ? 2 * n - 1 - k : -1;
+                const int xn = xr + dx, yn = yr + dy;
+                av = nb_available_wh(xn << sub, yn << sub, xcl, ycl, X.x0, X.y0, X.w, X.h, X.ctb, X.flags);
+                int v = 0;
+                if (av) v = yn < 0 ? top[xn] : (xn < 0 ? left[yn] : interior[yn * ist + xn]);
+                L.ref[0][k] = (uint16_t)v;
+            }
+            m[jj] = __ballot(av);
+        }
+        constexpr unsigned long long full0 = nref >= 64 ? ~0ull : ((1ull << (nref & 63)) - 1ull);
+        constexpr unsigned long long full1 = nref >= 128 ? ~0ull : (nref > 64 ? ((1ull << ((nref - 64) & 63)) - 1ull) : 0ull);
+        constexpr unsigned long long full2 = nref > 128 ? 1ull : 0ull;
+        const bool all = m[0] == full0 && m[1] == full1 && m[2] == full2;
+        bool filt = false;
+        if (n != 4 && c == 0 && mode != 1) {
+            const int dist = min(abs(mode - 26), abs(mode - 10));
+            filt = dist > (n == 8 ? 7 : (n == 16 ? 1 : 0));
+        }
+        wave_sync();
+        const uint16_t* R = L.ref[0];
+        int dcs = 0;
+        if (!all || filt || mode == 1) {
+            // ---- B: substitution (8.4.4.2.2) + filtering (8.4.4.2.3) -> ref[1] ------------
+            const bool any = (m[0] | m[1] | m[2]) != 0ull;
+            const int half = 1 << (bd - 1);
+            auto sval = [&](int i) -> int {
+                if (all) return (int)L.ref[0][i];
+                const int s = subst_src(i, m[0], m[1], m[2]);
+                return s < 0 ? half : (int)L.ref[0][s];
+            };
+            bool strong = false;
+            int corner = 0, bl = 0, tr = 0;
+            if (n == 32 && filt && X.strong) {
+                corner = sval(2 * n); bl = sval(0); tr = sval(4 * n);
+                strong = abs(corner + tr - 2 * sval(3 * n)) < (1 << (bd - 5)) &&
+                         abs(corner + bl - 2 * sval(n)) < (1 << (bd - 5));
+            }
+#pragma unroll
+            for (int jj = 0; jj < NCH; ++jj) {
+                const int k = lane + 64 * jj;
+                if (k < nref) {
+                    const int sk = any ? sval(k) : half;
+                    int f = sk;
+                    if (filt && k > 0 && k < 4 * n) {
+                        if (strong) {
+                            f = k == 2 * n ? corner
+                              : (k < 2 * n ? ((63 - (2 * n - 1 - k)) * corner + (2 * n - k) * bl + 32) >> 6
+                                           : ((63 - (k - 2 * n - 1)) * corner + (k - 2 * n) * tr + 32) >> 6);
+                        } else {
+                            f = (sval(k - 1) + 2 * sk + sval(k + 1) + 2) >> 2;
+                        }
+                    }
+                    L.ref[1][k] = (uint16_t)f;
+                    if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) dcs += sk;
+                }
+            }
+            wave_sync();
+            R = L.ref[1];
+        }
+        // ---- C: prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ----------------
+        if (mode == 0) {
+            const int trs = R[3 * n + 1], bls = R[n - 1];
+            const int ly = R[2 * n - 1 - sy];
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                const int x = sx + i;
+                put(i, ((n - 1 - x) * ly + (x + 1) * trs + (n - 1 - sy) * R[2 * n + 1 + x] + (sy + 1) * bls + n) >> (LOG2 + 1));
+            }
+        } else if (mode == 1) {
+            const int dc = (__ockl_wfred_add_i32(dcs) + n) >> (LOG2 + 1);
+            const bool edge = c == 0 && n < 32;
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                const int x = sx + i;
+                int v = dc;
+                if (edge) {
+                    if (x == 0 && sy == 0) v = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
+                    else if (sy == 0) v = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
+                    else if (x == 0) v = (R[2 * n - 1 - sy] + 3 * dc + 2) >> 2;
+                }
+                put(i, v);
+            }
+        } else if (mode >= 18) {                                    // vertical family
+            const int ang = c_angle[mode];
+            const int inv = c_inv_angle[mode];
+            const int idx = ((sy + 1) * ang) >> 5, fact = ((sy + 1) * ang) & 31;
+            auto refk = [&](int r) { return r >= 0 ? 2 * n + r : 2 * n - ((r * inv + 128) >> 8); };
+            const bool bflt = mode == 26 && c == 0 && n < 32;
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                const int x = sx + i;
+                const int r0 = x + idx + 1;
+                int v = R[refk(r0)];
+                if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
+                if (bflt && x == 0) v = clip_pel((int)R[2 * n + 1] + (((int)R[2 * n - 1 - sy] - (int)R[2 * n]) >> 1), maxv);
+                put(i, v);
+            }
+        } else {                                                    // horizontal family
+            const int ang = c_angle[mode];
+            const int inv = c_inv_angle[mode];
+            auto refk = [&](int r) { return r >= 0 ? 2 * n - r : 2 * n + ((r * inv + 128) >> 8); };
+            const bool bflt = mode == 10 && c == 0 && n < 32 && sy == 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                const int x = sx + i;
+                const int idx = ((x + 1) * ang) >> 5, fact = ((x + 1) * ang) & 31;
+                const int r0 = sy + idx + 1;
+                int v = R[refk(r0)];
+                if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
+                if (bflt) v = clip_pel((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), maxv);
+                put(i, v);
+            }
+        }
+    }
+    if (own) {
+        uint8_t* dst = interior + (yr + sy) * ist + xr + sx;
+        if constexpr (S == 16) *reinterpret_cast<uint4*>(dst) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+        else if constexpr (S == 4) *reinterpret_cast<uint32_t*>(dst) = outw[0];
+        else dst[0] = (uint8_t)outw[0];
+    }
+    wave_sync();
 }
 
 template <int W>
@@ -128,7 +324,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         if (r >= rows_total) break;
         const int j = r / g.hc, cy = r - j * g.hc;
         const int slot = j % fs_count, gen = j / fs_count;
-        const DevPic P = pics[b + j * G];
+        const DevPic P = gload(pics + b + j * G);
         // picture slot reuse: every row of picture j waits until picture j - fs_count (the
         // slot's previous occupant) has completed all its rows; those rows were dequeued
         // earlier and are held by running waves, so this wait always ends.
@@ -141,6 +337,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         const int* up_prog = &prog[slot * g.hc + (cy > 0 ? cy - 1 : 0)];
         const int tag = (j & 0xffff) << 16;
         if (lane == 0) __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const p265r_ctu* ctus = P.ctus;
 
         for (int cx = 0; cx < g.wc; ++cx) {
             // ---- wait for the row above (2-CTU lag) -------------------------------------
@@ -151,247 +348,99 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                         return (v & 0xffff0000) == tag && (v & 0xffff) >= need;
                     })) return;
             }
-            const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
+            CtuCtx X;
+            X.x0 = cx << g.ctb_log2; X.y0 = cy << g.ctb_log2;
+            X.w = g.w; X.h = g.h; X.cw = g.cw; X.ctb = ctb;
+            X.bd_l = g.bd[0]; X.bd_c = g.bd[1]; X.strong = g.strong;
             const int addr = cy * g.wc + cx;
-            const p265r_ctu me = P.ctus[addr];
+            // the CTU and its four causal neighbours: five independent loads, one wait
+            const p265r_ctu me = gload(ctus + addr);
+            const p265r_ctu nl = gload(ctus + (cx > 0 ? addr - 1 : addr));
+            const p265r_ctu nt_ = gload(ctus + (cy > 0 ? addr - g.wc : addr));
+            const p265r_ctu ntl = gload(ctus + (cx > 0 && cy > 0 ? addr - g.wc - 1 : addr));
+            const p265r_ctu ntr = gload(ctus + (cx + 1 < g.wc && cy > 0 ? addr - g.wc + 1 : addr));
             unsigned flags = 0;
-            if (cx > 0 && ctu_same_region(me, P.ctus[addr - 1])) flags |= 1u;
-            if (cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc])) flags |= 2u;
-            if (cx > 0 && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc - 1])) flags |= 4u;
-            if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc + 1])) flags |= 8u;
+            if (cx > 0 && ctu_same_region(me, nl)) flags |= 1u;
+            if (cy > 0 && ctu_same_region(me, nt_)) flags |= 2u;
+            if (cx > 0 && cy > 0 && ctu_same_region(me, ntl)) flags |= 4u;
+            if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, ntr)) flags |= 8u;
+            X.flags = flags;
 
             const int nt = me.tb_count;
-            const p265r_tb* tbs = P.tbs + me.tb_begin;
+            const uint4* trec = reinterpret_cast<const uint4*>(P.tbs + me.tb_begin);
             uint4 rec = make_uint4(0, 0, 0, 0);
-            if (lane < nt) rec = *reinterpret_cast<const uint4*>(tbs + lane);
+            if (lane < nt) rec = ld16(trec + lane);
 
-            // residual of TB t is loaded while TB t-1 is processed (2 x 16 B per lane, fixed shape)
-            auto load_res = [&](const TbRec& t, uint4& a, uint4& b2) {
-                const bool coded = t.flags & (P265R_TB_CBF | P265R_TB_PCM);
-                const int nn = 1 << (2 * t.log2);
+            // residual of TB t: always two aligned 16-B loads per lane (fixed shape, so the
+            // compiler's vmcnt bookkeeping stays exact; pools are padded by 64 B), issued
+            // while TB t-1 is processed.  TB offsets are multiples of 16 elements.
+            auto res_addr = [&](uint32_t w1, uint32_t off) {
+                const int lg = (int)(w1 & 0xff), fl = (int)(w1 >> 24);
+                const int nn = 1 << (2 * lg);
                 const int S = nn >= 64 ? (nn >> 6) : 1;
                 const int sidx = lane * S < nn ? lane * S : 0;
-                const int16_t* base = (t.flags & (P265R_TB_BYPASS | P265R_TB_PCM)) ? pool : resid;
-                if (coded) {
-                    const int16_t* rp = base + t.off + sidx;
-                    if (S == 16) { a = *reinterpret_cast<const uint4*>(rp); b2 = *reinterpret_cast<const uint4*>(rp + 8); }
-                    else if (S == 4) { const uint2 v = *reinterpret_cast<const uint2*>(rp); a = make_uint4(v.x, v.y, 0, 0); }
-                    else { a = make_uint4((uint32_t)(uint16_t)rp[0], 0, 0, 0); }
-                } else {
-                    a = make_uint4(0, 0, 0, 0); b2 = a;
-                }
+                const int16_t* base = (fl & (P265R_TB_BYPASS | P265R_TB_PCM)) ? pool : resid;
+                return reinterpret_cast<const uint4*>(base + off + (sidx & ~7));
             };
-            auto rec_of = [&](int t) {
-                if ((t & 63) == 0 && t) {          // next chunk of 64 records
-                    rec = make_uint4(0, 0, 0, 0);
-                    if (t + lane < nt) rec = *reinterpret_cast<const uint4*>(tbs + t + lane);
-                }
-                const int l = t & 63;
-                return tb_from_words(__builtin_amdgcn_readlane(rec.x, l), __builtin_amdgcn_readlane(rec.y, l),
-                                     __builtin_amdgcn_readlane(rec.z, l), __builtin_amdgcn_readlane(rec.w, l));
-            };
-
-            TbRec cur = nt ? rec_of(0) : TbRec{0, 0, 2, 0, 0, 0, 0};
+            uint32_t w0n = 0, w1n = 0, w3n = 0;
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-            if (nt) load_res(cur, ra, rb);
-
+            if (nt) {
+                w0n = __builtin_amdgcn_readlane(rec.x, 0);
+                w1n = __builtin_amdgcn_readlane(rec.y, 0);
+                w3n = __builtin_amdgcn_readlane(rec.w, 0);
+                const uint4* a = res_addr(w1n, w3n);
+                ra = ld16(a); rb = ld16(a + 1);
+            }
             for (int t = 0; t < nt; ++t) {
-                const TbRec tb = cur;
+                const uint32_t w0 = w0n, w1 = w1n;
                 const uint4 ca = ra, cb = rb;
-                if (t + 1 < nt) { cur = rec_of(t + 1); load_res(cur, ra, rb); }
-
-                const int c = tb.c;
-                const int sub = c ? 1 : 0;
-                const int log2 = tb.log2, n = 1 << log2;
-                const int xr = tb.x - (x0 >> sub), yr = tb.y - (y0 >> sub);
-                const int bd = g.bd[c];
-                const int maxv = (1 << bd) - 1;
-                uint8_t* interior = c ? L.c[c - 1] : L.y;
-                const int ist = c ? 32 : 64;
-                const uint8_t* top = line_up + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + (x0 >> sub);
-                const uint8_t* left = c ? L.cleft[c - 1] : L.yleft;
-                const int nn = n * n;
-                const int S = nn >= 64 ? (nn >> 6) : 1;
-                const bool own = lane * S < nn;
-                const int sidx = lane * S;
-                const int sy = sidx >> log2, sx = sidx & (n - 1);
-
-                int pred[16];
-                if (tb.flags & P265R_TB_PCM) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) pred[i] = 0;
-                } else {
-                    // ---- A: gather raw reference samples + availability ------------------
-                    const int nref = 4 * n + 1;
-                    const int xcl = xr << sub, ycl = yr << sub;
-                    unsigned long long m[3] = {0ull, 0ull, 0ull};
-#pragma unroll
-                    for (int jj = 0; jj < 3; ++jj) {
-                        if (jj * 64 < nref) {
-                            const int k = lane + 64 * jj;
-                            bool av = false;
-                            if (k < nref) {
-                                const int dx = k <= 2 * n ? -1 : k - 2 * n - 1;
-                                const int dy = k < 2 * n ? 2 * n - 1 - k : -1;
-                                const int xn = xr + dx, yn = yr + dy;
-                                av = nb_available(xn << sub, yn << sub, xcl, ycl, x0, y0, g, ctb, flags);
-                                int v = 0;
-                                if (av) v = yn < 0 ? top[xn] : (xn < 0 ? left[yn] : interior[yn * ist + xn]);
-                                L.ref[0][k] = (uint16_t)v;
-                            }
-                            m[jj] = __ballot(av);
-                        }
+                const bool coded = (w1 >> 24) & (P265R_TB_CBF | P265R_TB_PCM);
+                if (t + 1 < nt) {
+                    const int l = (t + 1) & 63;
+                    if (l == 0) {
+                        if (t + 1 + lane < nt) rec = ld16(trec + t + 1 + lane);
+                        else rec = make_uint4(0, 0, 0, 0);
                     }
-                    wave_sync();
-                    const int mode = tb.mode;
-                    bool filt = false;
-                    if (c == 0 && mode != 1 && n != 4) {
-                        const int dist = min(abs(mode - 26), abs(mode - 10));
-                        filt = dist > (n == 8 ? 7 : (n == 16 ? 1 : 0));
-                    }
-                    const bool any = (m[0] | m[1] | m[2]) != 0ull;
-                    const int half = 1 << (bd - 1);
-                    auto sval = [&](int i) -> int {
-                        const int s = subst_src(i, m[0], m[1], m[2]);
-                        return s < 0 ? half : (int)L.ref[0][s];
-                    };
-                    bool strong = false;
-                    int corner = 0, bl = 0, tr = 0;
-                    if (filt && g.strong && n == 32) {
-                        corner = sval(2 * n); bl = sval(0); tr = sval(4 * n);
-                        strong = abs(corner + tr - 2 * sval(3 * n)) < (1 << (bd - 5)) &&
-                                 abs(corner + bl - 2 * sval(n)) < (1 << (bd - 5));
-                    }
-                    int dcs = 0;
-                    // ---- B: substitution + filtering -> ref[1] ---------------------------
-#pragma unroll
-                    for (int jj = 0; jj < 3; ++jj) {
-                        if (jj * 64 < nref) {
-                            const int k = lane + 64 * jj;
-                            if (k < nref) {
-                                const int sk = any ? sval(k) : half;
-                                int f = sk;
-                                if (filt && k > 0 && k < 4 * n) {
-                                    if (strong) {
-                                        f = k == 2 * n ? corner
-                                          : (k < 2 * n ? ((63 - (2 * n - 1 - k)) * corner + (2 * n - k) * bl + 32) >> 6
-                                                       : ((63 - (k - 2 * n - 1)) * corner + (k - 2 * n) * tr + 32) >> 6);
-                                    } else {
-                                        f = (sval(k - 1) + 2 * sk + sval(k + 1) + 2) >> 2;
-                                    }
-                                }
-                                L.ref[1][k] = (uint16_t)f;
-                                if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) dcs += sk;
-                            }
-                        }
-                    }
-                    wave_sync();
-                    const uint16_t* R = L.ref[1];
-                    // ---- C: prediction -----------------------------------------------------
-                    if (mode == 0) {
-                        const int trs = R[3 * n + 1], bls = R[n - 1];
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            if (i < S) {
-                                const int x = sx + i, y = sy;
-                                pred[i] = ((n - 1 - x) * R[2 * n - 1 - y] + (x + 1) * trs +
-                                           (n - 1 - y) * R[2 * n + 1 + x] + (y + 1) * bls + n) >> (log2 + 1);
-                            }
-                        }
-                    } else if (mode == 1) {
-                        const int dc = (__ockl_wfred_add_i32(dcs) + n) >> (log2 + 1);
-                        const bool edge = c == 0 && n < 32;
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            if (i < S) {
-                                const int x = sx + i, y = sy;
-                                int v = dc;
-                                if (edge) {
-                                    if (x == 0 && y == 0) v = (R[2 * n - 1] + 2 * dc + R[2 * n + 1] + 2) >> 2;
-                                    else if (y == 0) v = (R[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                                    else if (x == 0) v = (R[2 * n - 1 - y] + 3 * dc + 2) >> 2;
-                                }
-                                pred[i] = v;
-                            }
-                        }
-                    } else {
-                        const int ang = c_angle[mode];
-                        const int inv = c_inv_angle[mode];
-                        const bool vert = mode >= 18;
-                        const int dir = vert ? 1 : -1;
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            if (i < S) {
-                                const int x = sx + i, y = sy;
-                                const int a = vert ? y : x, bb = vert ? x : y;
-                                const int idx = ((a + 1) * ang) >> 5, fact = ((a + 1) * ang) & 31;
-                                const int r0 = bb + idx + 1;
-                                const int k0 = r0 >= 0 ? 2 * n + dir * r0 : 2 * n - dir * ((r0 * inv + 128) >> 8);
-                                int v = R[k0];
-                                if (fact) {
-                                    const int r1 = r0 + 1;
-                                    const int k1 = r1 >= 0 ? 2 * n + dir * r1 : 2 * n - dir * ((r1 * inv + 128) >> 8);
-                                    v = ((32 - fact) * v + fact * (int)R[k1] + 16) >> 5;
-                                }
-                                if (c == 0 && n < 32) {
-                                    if (mode == 26 && x == 0)
-                                        v = min(max((int)R[2 * n + 1] + (((int)R[2 * n - 1 - y] - (int)R[2 * n]) >> 1), 0), maxv);
-                                    if (mode == 10 && y == 0)
-                                        v = min(max((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), 0), maxv);
-                                }
-                                pred[i] = v;
-                            }
-                        }
-                    }
+                    w0n = __builtin_amdgcn_readlane(rec.x, l);
+                    w1n = __builtin_amdgcn_readlane(rec.y, l);
+                    w3n = __builtin_amdgcn_readlane(rec.w, l);
+                    const uint4* a = res_addr(w1n, w3n);
+                    ra = ld16(a); rb = ld16(a + 1);
                 }
-                // ---- reconstruction into the wave's CTU image -------------------------------
-                if (own) {
-                    const uint32_t w8[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
-                    auto resv = [&](int i) { return (int)(int16_t)(w8[i >> 1] >> ((i & 1) * 16)); };
-                    uint8_t* dst = interior + (yr + sy) * ist + xr + sx;
-                    if (S == 16) {
-                        uint32_t w[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            uint32_t v = 0;
-#pragma unroll
-                            for (int bb = 0; bb < 4; ++bb)
-                                v |= (uint32_t)min(max(pred[q * 4 + bb] + resv(q * 4 + bb), 0), maxv) << (8 * bb);
-                            w[q] = v;
-                        }
-                        *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
-                    } else if (S == 4) {
-                        uint32_t v = 0;
-#pragma unroll
-                        for (int bb = 0; bb < 4; ++bb) v |= (uint32_t)min(max(pred[bb] + resv(bb), 0), maxv) << (8 * bb);
-                        *reinterpret_cast<uint32_t*>(dst) = v;
-                    } else {
-                        dst[0] = (uint8_t)min(max(pred[0] + resv(0), 0), maxv);
-                    }
+                const uint4 za = coded ? ca : make_uint4(0, 0, 0, 0);
+                const uint4 zb = coded ? cb : make_uint4(0, 0, 0, 0);
+                const int tx = (int)(w0 & 0xffff), ty = (int)(w0 >> 16);
+                const int lg = (int)(w1 & 0xff), c = (int)((w1 >> 8) & 0xff);
+                const int mode = (int)((w1 >> 16) & 0xff), fl = (int)(w1 >> 24);
+                switch (lg) {
+                    case 2: recon_tb<2>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
+                    case 3: recon_tb<3>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
+                    case 4: recon_tb<4>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
+                    default: recon_tb<5>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
                 }
-                wave_sync();
             }
 
             // ---- publish the CTU: planes (HBM), bottom line (LDS), right column (LDS) ----------
+#pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const int sub = c ? 1 : 0;
                 const int cs = ctb >> sub;
                 const int Wd = c ? g.cw : g.w, Ht = c ? g.ch : g.h;
-                const int xb = x0 >> sub, yb = y0 >> sub;
+                const int xb = X.x0 >> sub, yb = X.y0 >> sub;
                 const int wv = min(cs, Wd - xb), hv = min(cs, Ht - yb);
-                const uint8_t* src = c ? L.c[c - 1] : L.y;
+                const uint8_t* src = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
                 const int ist = c ? 32 : 64;
-                uint8_t* plane = P.rec[c];
+                P265R_GLOBAL uint8_t* plane = gptr_w(P.rec[c]);
                 const int st = g.stride[c];
                 const int gpr = wv >> 2;
                 for (int e = lane; e < gpr * hv; e += 64) {
                     const int yy = e / gpr, xx = (e - yy * gpr) << 2;
-                    *reinterpret_cast<uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
+                    *reinterpret_cast<P265R_GLOBAL uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
                         *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
                 }
                 unsigned char* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
                 if (lane < wv) lc[lane] = src[(hv - 1) * ist + lane];
-                uint8_t* lf = c ? L.cleft[c - 1] : L.yleft;
+                uint8_t* lf = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
                 if (lane < hv) lf[lane] = src[lane * ist + wv - 1];
             }
             if (lane == 0)

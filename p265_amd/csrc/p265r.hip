@@ -290,8 +290,9 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t o_err = off; off = align_up(off + 256, 256);
     const size_t o_ctus = off; off = align_up(off + sizeof(p265r_ctu) * nc * (size_t)n_pics, 256);
     const size_t o_tbs = off; off = align_up(off + sizeof(p265r_tb) * n_tbs_total, 256);
-    const size_t o_pool = off; off = align_up(off + sizeof(int16_t) * pool_total, 256);
-    const size_t o_res = off; off = align_up(off + sizeof(int16_t) * pool_total, 256);
+    // both pools padded by 64 B: the intra kernel reads fixed-shape 32-B runs
+    const size_t o_pool = off; off = align_up(off + sizeof(int16_t) * pool_total + 64, 256);
+    const size_t o_res = off; off = align_up(off + sizeof(int16_t) * pool_total + 64, 256);
     size_t o_jobs[RC_NUM];
     for (int c = 0; c < RC_NUM; ++c) { o_jobs[c] = off; off = align_up(off + sizeof(ResJob) * n_jobs[c], 256); }
     size_t o_nf = off;
