@@ -5,7 +5,7 @@ HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -shared -Wall -Wno-unuse
 SRC := p265_amd/csrc/p265r.hip
 HDR := $(wildcard p265_amd/csrc/*.h) include/p265r.h
 
-all: p265_amd/libp265r.so
+all: p265_amd/libp265r.so oracle
 
 p265_amd/libp265r.so: $(SRC) $(HDR)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)

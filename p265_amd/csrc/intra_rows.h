@@ -40,6 +40,18 @@ __device__ __forceinline__ uint4 ld16(const void* p) {
     const u32x4_t v = *reinterpret_cast<const P265R_GLOBAL u32x4_t*>(gptr(p));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// make every 32-bit word of a (wave-uniform) struct provably uniform: SGPRs, scalar branches
+template <typename T>
+__device__ __forceinline__ T uniform(const T& v) {
+    static_assert(sizeof(T) % 4 == 0, "32-bit granules");
+    uint32_t w[sizeof(T) / 4];
+    __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
+    T o;
+    __builtin_memcpy(&o, w, sizeof(T));
+    return o;
+}
 // copy a POD struct out of global memory with global (not flat) loads
 template <typename T>
 __device__ __forceinline__ T gload(const T* p) {
@@ -282,7 +294,14 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                                                            const int16_t* __restrict__ pool,
                                                            const int16_t* __restrict__ resid,
                                                            Geo g, int n_pics, int fs_count,
-                                                           int* __restrict__ err_flag) {
+                                                           int* __restrict__ err_flag,
+                                                           int* __restrict__ dbg) {
+    // debug trace (P265R_DEBUG_SYNC=1): host-mapped words, one per wave
+#if defined(P265R_DBG_NOTRACE)
+#define P265R_TRACE(code) do { } while (0)
+#else
+#define P265R_TRACE(code) do { if (dbg && lane == 0) __hip_atomic_store(dbg + blockIdx.x * W + wave, (code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     RowCtrl& ctl = *reinterpret_cast<RowCtrl*>(smem);
     const int wave = threadIdx.x >> 6;
@@ -303,34 +322,37 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
     const int n_my = b < n_pics ? (n_pics - b + G - 1) / G : 0;
     const int rows_total = n_my * g.hc;
     const int ctb = 1 << g.ctb_log2;
-    // bounded spin-wait on an LDS word; false = gave up (error published, caller returns)
+    // bounded spin-wait on an LDS word; false = gave up (error published, caller bails out).
+    // Every condition is made wave-uniform (readfirstlane) so the loops are scalar loops.
     auto wait_until = [&](auto ready) -> bool {
-        long spins = 0;
-        for (;;) {
-            if (ready()) return true;
-            if (__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1l << 24)) {                    // never hang the GPU
-                if (lane == 0) { ctl.error = 1; atomicOr(err_flag, 1); }
+        for (int spins = 0; spins < (1 << 24); ++spins) {
+            if (__builtin_amdgcn_readfirstlane((int)ready())) return true;
+            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 return false;
-            }
+            __builtin_amdgcn_s_sleep(1);
         }
+        if (lane == 0) { __hip_atomic_store(&ctl.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); atomicOr(err_flag, 1); }
+        return false;                                       // never hang the GPU
     };
+    bool failed = false;
 
+    P265R_TRACE(1);
     for (;;) {
         int r = 0;
         if (lane == 0) r = __hip_atomic_fetch_add(&ctl.next_row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         r = __builtin_amdgcn_readfirstlane(r);
-        if (r >= rows_total) break;
+        if (r >= rows_total || failed) break;
+        P265R_TRACE(2 | (r << 8));
         const int j = r / g.hc, cy = r - j * g.hc;
         const int slot = j % fs_count, gen = j / fs_count;
-        const DevPic P = gload(pics + b + j * G);
+        const DevPic P = uniform(gload(pics + b + j * G));
         // picture slot reuse: every row of picture j waits until picture j - fs_count (the
         // slot's previous occupant) has completed all its rows; those rows were dequeued
         // earlier and are held by running waves, so this wait always ends.
         if (!wait_until([&] {
                 return __hip_atomic_load(&ctl.done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen * g.hc;
-            })) return;
+            })) { failed = true; break; }
+        P265R_TRACE(3 | (r << 8));
         unsigned char* line_cur = lines + (size_t)(slot * 2 + (cy & 1)) * line_bytes;
         const unsigned char* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
         int* my_prog = &prog[slot * g.hc + cy];
@@ -346,19 +368,20 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 if (!wait_until([&] {
                         const int v = __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                         return (v & 0xffff0000) == tag && (v & 0xffff) >= need;
-                    })) return;
+                    })) { failed = true; break; }
             }
+            P265R_TRACE(4 | (cx << 8) | (r << 16));
             CtuCtx X;
             X.x0 = cx << g.ctb_log2; X.y0 = cy << g.ctb_log2;
             X.w = g.w; X.h = g.h; X.cw = g.cw; X.ctb = ctb;
             X.bd_l = g.bd[0]; X.bd_c = g.bd[1]; X.strong = g.strong;
             const int addr = cy * g.wc + cx;
             // the CTU and its four causal neighbours: five independent loads, one wait
-            const p265r_ctu me = gload(ctus + addr);
-            const p265r_ctu nl = gload(ctus + (cx > 0 ? addr - 1 : addr));
-            const p265r_ctu nt_ = gload(ctus + (cy > 0 ? addr - g.wc : addr));
-            const p265r_ctu ntl = gload(ctus + (cx > 0 && cy > 0 ? addr - g.wc - 1 : addr));
-            const p265r_ctu ntr = gload(ctus + (cx + 1 < g.wc && cy > 0 ? addr - g.wc + 1 : addr));
+            const p265r_ctu me = uniform(gload(ctus + addr));
+            const p265r_ctu nl = uniform(gload(ctus + (cx > 0 ? addr - 1 : addr)));
+            const p265r_ctu nt_ = uniform(gload(ctus + (cy > 0 ? addr - g.wc : addr)));
+            const p265r_ctu ntl = uniform(gload(ctus + (cx > 0 && cy > 0 ? addr - g.wc - 1 : addr)));
+            const p265r_ctu ntr = uniform(gload(ctus + (cx + 1 < g.wc && cy > 0 ? addr - g.wc + 1 : addr)));
             unsigned flags = 0;
             if (cx > 0 && ctu_same_region(me, nl)) flags |= 1u;
             if (cy > 0 && ctu_same_region(me, nt_)) flags |= 2u;
@@ -420,6 +443,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 }
             }
 
+            P265R_TRACE(5 | (cx << 8) | (r << 16));
             // ---- publish the CTU: planes (HBM), bottom line (LDS), right column (LDS) ----------
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -447,8 +471,13 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             wave_sync();
         }
+        if (failed) break;
         if (lane == 0) __hip_atomic_fetch_add(&ctl.done[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        P265R_TRACE(6 | (r << 8));
     }
+    P265R_TRACE(7);
+    // all stores of this wave are issued before it ends (compiler barrier)
+    asm volatile("" ::: "memory");
 }
 
 }  // namespace p265r

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <cstring>
 #include <new>
 #include <string>
@@ -78,6 +79,7 @@ struct p265r_ctx {
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
     int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16)
     int num_cus = 256;
+    bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
 };
 
 struct p265r_batch {
@@ -145,8 +147,28 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds));
     if (per_cu < 1) return P265R_EUNSUPPORTED;
     const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
-    fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, b->d_err);
+    int* dbg = nullptr;
+    if (ctx->debug_sync) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * grid * W, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(dbg, 0, sizeof(int) * grid * W);
+        fprintf(stderr, "[p265r] rows kernel W=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, grid, lds, fs, per_cu);
+    }
+    fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, b->d_err, dbg);
     HIP_TRY(hipGetLastError());
+    if (dbg) {
+        for (int it = 0; it < 100; ++it) {
+            if (hipStreamQuery(ctx->stream) == hipSuccess) break;
+            struct timespec ts{0, 100000000};
+            nanosleep(&ts, nullptr);
+            if (it == 99) {
+                fprintf(stderr, "[p265r] rows kernel still running after 10 s; wave trace:\n");
+                for (int i = 0; i < grid * W && i < 64; ++i) fprintf(stderr, "  wg %d wave %d: code %d (0x%x)\n", i / W, i % W, dbg[i] & 0xff, dbg[i]);
+                fflush(stderr);
+                std::abort();
+            }
+        }
+        (void)hipHostFree(dbg);
+    }
     return P265R_OK;
 }
 
@@ -215,6 +237,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.nf_w = (g.w + 7) / 8;
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
+    if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 8 || w == 16) ctx->row_waves = w;
@@ -413,6 +436,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         ++tm.residual_launches;
     }
     HIP_TRY(hipGetLastError());
+    if (ctx->debug_sync) { fprintf(stderr, "[p265r] residual phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] residual phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
     // ---- intra wavefront ---------------------------------------------------------------
     if (ctx->schedule == 1) {
@@ -432,6 +456,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         ++tm.intra_launches;
     }
     HIP_TRY(hipGetLastError());
+    if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // ---- SAO -----------------------------------------------------------------------
     if (b->sao) {
