@@ -331,15 +331,17 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 return false;
             __builtin_amdgcn_s_sleep(1);
         }
-        if (lane == 0) { __hip_atomic_store(&ctl.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); atomicOr(err_flag, 1); }
+        __hip_atomic_store(&ctl.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // all lanes, same value
+        atomicOr(err_flag, 1);
         return false;                                       // never hang the GPU
     };
     bool failed = false;
 
     P265R_TRACE(1);
     for (;;) {
-        int r = 0;
-        if (lane == 0) r = __hip_atomic_fetch_add(&ctl.next_row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // row queue: the whole wave executes the atomic (no lane-0 branch inside the loop);
+        // only lane 0 contributes, so the wave takes exactly one row
+        int r = __hip_atomic_fetch_add(&ctl.next_row, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         r = __builtin_amdgcn_readfirstlane(r);
         if (r >= rows_total || failed) break;
         P265R_TRACE(2 | (r << 8));
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         int* my_prog = &prog[slot * g.hc + cy];
         const int* up_prog = &prog[slot * g.hc + (cy > 0 ? cy - 1 : 0)];
         const int tag = (j & 0xffff) << 16;
-        if (lane == 0) __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         const p265r_ctu* ctus = P.ctus;
 
         for (int cx = 0; cx < g.wc; ++cx) {
@@ -467,12 +469,11 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 uint8_t* lf = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
                 if (lane < hv) lf[lane] = src[lane * ist + wv - 1];
             }
-            if (lane == 0)
-                __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             wave_sync();
         }
         if (failed) break;
-        if (lane == 0) __hip_atomic_fetch_add(&ctl.done[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&ctl.done[slot], lane == 0 ? 1 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         P265R_TRACE(6 | (r << 8));
     }
     P265R_TRACE(7);
