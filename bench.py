@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: reconstructed 1080p all-intra CTUs/s on MI355X (BASELINE.json metric).
 
-A "step" is one pass of the hot path (residual -> intra wavefront -> SAO) over one
-batch of synthetic 1080p all-intra pictures already resident in HBM (config 3 shape,
-with SAO as in config 4).  N GPUs: one process per GPU (torch.distributed.run), each
-rank decodes its own batch of independent frames (weak scaling, no data-path
-collective); the SPS/PPS parameter POD is broadcast from rank 0 over RCCL once,
-outside the timed region.  Rank 0 prints ONE JSON line.
+A "step" is one pass of the hot path -- residual (dequant + inverse DCT/DST) -> intra
+prediction + reconstruction -> SAO -- over one batch of synthetic 1080p all-intra
+pictures whose records are already resident in HBM (config C3 shape with SAO on, i.e.
+C4's per-GPU work).  N GPUs: one process per GPU (torch.distributed.run); each rank
+decodes its own batch of independent pictures (weak scaling, no data-path collective);
+the 32-byte SPS/PPS POD is broadcast from rank 0 over RCCL once, outside the timed
+region.  Rank 0 prints ONE JSON line.
 
-    python bench.py --gpus 1 --steps 10 --warmup 3
+    python bench.py                       # N=1, defaults finish in ~1-2 minutes
+    torchrun --nproc-per-node 8 bench.py --gpus 8
 """
 import argparse
 import json
@@ -16,12 +18,11 @@ import os
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = "reconstructed CTUs/sec (1080p all-intra) + achieved HBM GB/s vs peak"
 
 
 def parse():
@@ -29,19 +30,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=64, help="1080p pictures per GPU per step")
+    ap.add_argument("--frames", type=int, default=512, help="1080p pictures per GPU per step")
     ap.add_argument("--unique", type=int, default=4, help="distinct synthetic pictures per rank (replicated)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
 def algorithmic_bytes(pics):
-    """B = 2C + 16 N_TB + 16 N_CU + 3 S + 32 N_CTU, per picture list.
+    """B = 2C + 16 N_TB + 16 N_CU + 3 S + 32 N_CTU per picture.
 
-    N_CU is not carried by the records (the TB records hold every CU-level field the
-    path reads), so its 16 B term is taken as 0; S counts luma + chroma samples.
-    Returns (whole-path bytes, intra-kernel bytes, residual-kernel bytes, sao bytes).
+    N_CU is not carried by the records (each TB record holds the CU-level fields the path
+    reads), so the 16 N_CU term is 0; S counts luma + chroma samples.  Also returns the
+    per-kernel figures: intra (2C residual read + 16 N_TB + S recon write + 32 N_CTU),
+    residual (2C read + 2C write + 8 B job record per coded TB), SAO (2S + 32 N_CTU).
     """
     tot = intra = resid = sao = 0
     for p in pics:
@@ -49,34 +51,43 @@ def algorithmic_bytes(pics):
         ntb, nctu = len(p.tbs), len(p.ctus)
         s = p.meta["samples"]
         tot += 2 * c + 16 * ntb + 3 * s + 32 * nctu
-        intra += 2 * c + 16 * ntb + s + 32 * nctu          # residual read, TB/CTU records, recon write
-        resid += 4 * c + 8 * ntb                           # level read + residual write (+ job records)
+        intra += 2 * c + 16 * ntb + s + 32 * nctu
+        resid += 4 * c + 8 * int(((p.tbs["flags"] & 1) != 0).sum())
         sao += 2 * s + 32 * nctu
     return tot, intra, resid, sao
 
 
+def cpu_baseline(params, uniq, budget_s):
+    """CPU oracle (oracle/recon_oracle.c, test infrastructure used here only as the reported
+    baseline) on a bounded sample of the same workload: whole synthetic 1080p pictures,
+    repeated until ~budget_s of wall time, OpenMP over pictures on the host cores."""
+    from oracle import c_oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    c_oracle.decode(params, uniq[:1], threads=1, with_recon=False)           # warm
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        batch = [uniq[i % len(uniq)] for i in range(threads * 2)]
+        c_oracle.decode(params, batch, threads=threads, with_recon=False)
+        n += len(batch)
+    dt = time.perf_counter() - t0
+    ctus = n * len(uniq[0].ctus)
+    return {"value": round(ctus / dt, 1), "unit": "CTU/s", "cores": threads, "kind": "port",
+            "sample": "oracle/recon_oracle.c (scalar C restatement, OpenMP over pictures): %d synthetic 1080p "
+                      "pictures = %d CTUs in %.1f s" % (n, ctus, dt)}
+
+
 def main():
     a = parse()
-    import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
-    from p265_amd import recon, synth
+    import torch  # noqa: F401  (loads the HIP runtime libp265r.so binds to; see p265_amd/_lib.py)
+    from p265_amd import dist, recon, synth
     from p265_amd import records as R
 
+    rank, world, local = dist.init("nccl")
     params = R.make_params(pic_width=1920, pic_height=1080)
-    if world > 1:                                   # SPS/PPS POD broadcast over RCCL (xGMI)
-        blob = torch.from_numpy(np.frombuffer(params.tobytes(), np.uint8).copy()).cuda()
-        dist.broadcast(blob, src=0)
-        params = np.frombuffer(blob.cpu().numpy().tobytes(), R.PARAMS_DTYPE)[0]
+    params = dist.broadcast_params(params)                  # RCCL broadcast of the SPS/PPS POD
 
     t0 = time.time()
-    uniq = [synth.make_picture(params, 265 + 3 + 1000 * rank + i, perf=True) for i in range(a.unique)]
+    uniq = [synth.make_picture(params, 268 + 1000 * rank + i, perf=True) for i in range(a.unique)]
     for p in uniq:
         p.meta["samples"] = 1920 * 1080 * 3 // 2
     pics = [uniq[i % a.unique] for i in range(a.frames)]
@@ -89,73 +100,56 @@ def main():
         ctx.run(batch)
     ctx.sync()
     ctx.set_timing(True)
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     ctx.sync()
     t_start = time.perf_counter()
     acc = {"total_ms": 0.0, "residual_ms": 0.0, "intra_ms": 0.0, "sao_ms": 0.0, "intra_launches": 0}
     for _ in range(a.steps):
         ctx.run(batch)
-        tm = ctx.last_timings()            # waits on this run's last event (HIP events, ctx stream)
+        tm = ctx.last_timings()            # HIP events on the context's own stream
         for k in acc:
             acc[k] += tm[k]
     ctx.sync()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    dist.barrier()
+    elapsed = dist.max_over_ranks(time.perf_counter() - t_start)
 
     total_ctus = world * a.frames * n_ctu * a.steps
     value = total_ctus / elapsed
     tot_b, intra_b, res_b, sao_b = algorithmic_bytes(pics)
-    avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     launches_per_step = acc["intra_launches"] / a.steps
+    avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     bytes_per_launch = intra_b / launches_per_step
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     out = {
-        "metric": "reconstructed CTUs/sec (1080p all-intra) + achieved HBM GB/s vs peak",
+        "metric": METRIC,
         "value": round(value, 1), "unit": "CTU/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8/int16", "data": "synthetic (seeded all-intra records, sanity.bin statistics)",
-        "config": {"workload": "C3/C4: 1080p all-intra + SAO, %d frames per GPU per step (%d distinct)" % (a.frames, a.unique),
-                   "frames_per_gpu": a.frames, "ctus_per_frame": n_ctu, "ctb": 64,
-                   "parallelism": "frame-sharded x%d" % world},
-        "roofline": {"bound": "hbm", "kernel": "intra_step_kernel", "achieved": round(achieved, 3),
+        "vs_baseline": None, "dtype": "u8 samples / int16 coefficients (integer)",
+        "data": "synthetic: seeded all-intra records with sanity.bin statistics (p265_amd/synth.py)",
+        "config": {"workload": "C3/C4: 1080p all-intra + SAO, %d pictures per GPU per step (%d distinct)" % (a.frames, a.unique),
+                   "pictures_per_gpu": a.frames, "ctus_per_picture": n_ctu, "ctb": 64,
+                   "parallelism": "picture-sharded x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 5)},
+                     "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
+                     "note": "latency/issue-bound dependency chain; see DESIGN.md §4 and profiles/"},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
         "phase_gbs": {"residual": round(res_b / (acc["residual_ms"] / a.steps * 1e-3) / 1e9, 1),
                       "sao": round(sao_b / (acc["sao_ms"] / a.steps * 1e-3) / 1e9, 1) if acc["sao_ms"] else None,
-                      "whole_path": round(tot_b / (elapsed / a.steps) / 1e9, 2)},
+                      "whole_path_algorithmic": round(tot_b / (elapsed / a.steps) / 1e9, 2)},
         "setup_s": round(gen_s, 1),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(params, uniq[0], a.cpu_baseline_seconds)
+        out["cpu_baseline"] = cpu_baseline(params, uniq, a.cpu_baseline_seconds)
     batch.free()
     ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.destroy_process_group()
-
-
-def cpu_baseline(params, pic, budget_s):
-    """Time the CPU oracle (test infrastructure, used here only as the reported baseline)
-    on a bounded sample: whole CTUs of one 1080p picture, as many as fit the budget."""
-    from oracle import recon_oracle as O
-    from p265_amd import records as R
-    pd = R.params_dict(params)
-    t = time.perf_counter()
-    O.decode_picture(pd, pic.as_oracle_dict())
-    dt = time.perf_counter() - t
-    n = len(pic.ctus)
-    return {"value": round(n / dt, 2), "unit": "CTU/s", "cores": 1, "kind": "port",
-            "sample": "oracle/recon_oracle.py (numpy restatement), 1 synthetic 1080p frame = %d CTUs, %.1f s" % (n, dt)}
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

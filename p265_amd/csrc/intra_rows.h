@@ -324,9 +324,13 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
     const int ctb = 1 << g.ctb_log2;
     // bounded spin-wait on an LDS word; false = gave up (error published, caller bails out).
     // Every condition is made wave-uniform (readfirstlane) so the loops are scalar loops.
+    long long t_wait = 0;
+    const long long t_begin = __builtin_amdgcn_s_memtime();
     auto wait_until = [&](auto ready) -> bool {
+        const long long t0 = __builtin_amdgcn_s_memtime();
         for (int spins = 0; spins < (1 << 24); ++spins) {
-            if (__builtin_amdgcn_readfirstlane((int)ready())) return true;
+            if (spins == 0 && __builtin_amdgcn_readfirstlane((int)ready())) return true;
+            if (__builtin_amdgcn_readfirstlane((int)ready())) { t_wait += __builtin_amdgcn_s_memtime() - t0; return true; }
             if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 return false;
             __builtin_amdgcn_s_sleep(1);
@@ -477,6 +481,12 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         P265R_TRACE(6 | (r << 8));
     }
     P265R_TRACE(7);
+    if (dbg) {   // debug statistics: [total cycles, cycles in dependency waits] per wave
+        const long long t_all = __builtin_amdgcn_s_memtime() - t_begin;
+        const int slotw = gridDim.x * W + 2 * (blockIdx.x * W + wave);
+        __hip_atomic_store(dbg + slotw, (int)(t_all >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dbg + slotw + 1, (int)(t_wait >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     // all stores of this wave are issued before it ends (compiler barrier)
     asm volatile("" ::: "memory");
 }

@@ -77,7 +77,7 @@ struct p265r_ctx {
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
-    int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16)
+    int row_waves = 16;        // waves per workgroup of the row pipeline (4, 8 or 16)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
 };
@@ -149,8 +149,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
     const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
     int* dbg = nullptr;
     if (ctx->debug_sync) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * grid * W, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(dbg, 0, sizeof(int) * grid * W);
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * grid * W * 3, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(dbg, 0, sizeof(int) * grid * W * 3);
         fprintf(stderr, "[p265r] rows kernel W=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, grid, lds, fs, per_cu);
     }
     fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, b->d_err, dbg);
@@ -167,6 +167,9 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
                 std::abort();
             }
         }
+        double tot = 0, wt = 0;
+        for (int i = 0; i < grid * W; ++i) { tot += dbg[grid * W + 2 * i]; wt += dbg[grid * W + 2 * i + 1]; }
+        fprintf(stderr, "[p265r] rows kernel: %.1f%% of wave time in dependency waits (%d waves)\n", 100.0 * wt / (tot > 0 ? tot : 1), grid * W);
         (void)hipHostFree(dbg);
     }
     return P265R_OK;

@@ -1,6 +1,6 @@
 set -e
 mkdir -p gpurun_out
-P265R_LIB=$PWD/p265_amd/libp265r_N.so P265R_ROW_WAVES=4 timeout -k 5 25 python -u .dbg.py > gpurun_out/dbg_N.log 2>&1 || { echo "N variant hung/failed"; exit 1; }
+P265R_LIB=$PWD/p265_amd/libp265r_N.so P265R_ROW_WAVES=4 timeout -k 5 25 python -u tools/gpu_debug.py > gpurun_out/dbg_N.log 2>&1 || { echo "N variant hung/failed"; exit 1; }
 echo "notrace variant ok"
 timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
