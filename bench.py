@@ -23,6 +23,27 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "reconstructed CTUs/sec (1080p all-intra) + achieved HBM GB/s vs peak"
+# rocprofv3 PMC summary of this same command (tools/profile_round.sh + tools/profile_summary.py);
+# its HBM traffic per intra launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction) fills roofline.traffic
+PROFILE = os.path.join(ROOT, "profiles", "LATEST")
+
+
+def measured_traffic(kernel_prefix, frames):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary, or None
+    when no summary exists for this batch size (PMC counters cannot be read inside the run)."""
+    try:
+        tag = open(PROFILE).read().strip()
+        summ = json.load(open(os.path.join(ROOT, "profiles", tag, "summary.json")))
+        lines = open(os.path.join(ROOT, "profiles", tag, "bench.json")).read().splitlines()
+        meta = json.loads([ln for ln in lines if ln.startswith("{")][-1])
+    except (OSError, ValueError, IndexError):
+        return None, None
+    if int(meta.get("config", {}).get("pictures_per_gpu", -1)) != frames:
+        return None, tag
+    for name, row in summ.items():
+        if kernel_prefix in name and row.get("traffic_gb"):
+            return int(row["traffic_gb"] * 1e9), tag
+    return None, tag
 
 
 def parse():
@@ -122,6 +143,7 @@ def main():
     avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     bytes_per_launch = intra_b / launches_per_step
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    traffic, prof_tag = measured_traffic("intra_rows_kernel", a.frames)
     out = {
         "metric": METRIC,
         "value": round(value, 1), "unit": "CTU/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -132,7 +154,8 @@ def main():
                    "pictures_per_gpu": a.frames, "ctus_per_picture": n_ctu, "ctb": 64,
                    "parallelism": "picture-sharded x%d" % world},
         "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel", "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": ("profiles/%s/summary.json (rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)" % prof_tag) if traffic else None,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
                      "note": "latency/issue-bound dependency chain; see DESIGN.md §4 and profiles/"},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_round.sh output dir into profiles/<tag>/ (kept in git).
+
+FETCH_SIZE/WRITE_SIZE are KB per dispatch (rocprofv3); per MI355X_MICROARCH.md
+§HBM, FETCH_SIZE under-reports wide (16 B/lane) coalesced reads by exactly 2x on gfx950,
+so the corrected HBM traffic is 2*FETCH + WRITE for kernels whose loads are 16 B/lane
+(residual and intra kernels); the SAO kernel's byte loads are uncalibrated (raw shown).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def per_kernel(path):
+    rows = list(csv.DictReader(open(path)))
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    n = collections.defaultdict(collections.Counter)
+    for r in rows:
+        k = r["Kernel_Name"].split("(")[0]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        n[k][r["Counter_Name"]] += 1
+    return {k: {c: v / n[k][c] for c, v in d.items()} for k, d in agg.items()}
+
+
+def main(src, tag):
+    dst = os.path.join("profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    stats = list(csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))))
+    fe = per_kernel(os.path.join(src, "fetch", "fe_counter_collection.csv"))
+    wr = per_kernel(os.path.join(src, "write", "wr_counter_collection.csv"))
+    sq = per_kernel(os.path.join(src, "sq", "sq_counter_collection.csv"))
+    out = {}
+    lines = ["# rocprofv3 summary `%s` (bench.py --frames 512 --steps 3 --warmup 1, 1080p)" % tag, "",
+             "| kernel | calls | avg ms | FETCH KB | WRITE KB | corrected traffic GB (2F+W) | VALU/wave | SALU/wave | LDS/wave |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    for s in stats:
+        name = s["Name"].split("(")[0]
+        if name.startswith("__amd"):
+            continue
+        f, w = fe.get(name, {}).get("FETCH_SIZE", 0.0), wr.get(name, {}).get("WRITE_SIZE", 0.0)
+        q = sq.get(name, {})
+        waves = max(q.get("SQ_WAVES", 1.0), 1.0)
+        traffic = (2 * f + w) * 1024 / 1e9
+        out[name] = dict(calls=int(s["Calls"]), avg_ms=float(s["AverageNs"]) / 1e6, fetch_kb=f, write_kb=w,
+                         traffic_gb=traffic, **{k: v for k, v in q.items()})
+        lines.append("| %s | %s | %.4f | %.4g | %.4g | %.4g | %.4g | %.4g | %.4g |" % (
+            name, s["Calls"], float(s["AverageNs"]) / 1e6, f, w, traffic, q.get("SQ_INSTS_VALU", 0) / waves,
+            q.get("SQ_INSTS_SALU", 0) / waves, q.get("SQ_INSTS_LDS", 0) / waves))
+    lines += ["", "Counters per dispatch (SQ): see summary.json.  FETCH_SIZE correction: MI355X_MICROARCH.md §HBM."]
+    open(os.path.join(dst, "summary.md"), "w").write("\n".join(lines) + "\n")
+    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1, sort_keys=True)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
