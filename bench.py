@@ -28,7 +28,7 @@ METRIC = "reconstructed CTUs/sec (1080p all-intra) + achieved HBM GB/s vs peak"
 PROFILE = os.path.join(ROOT, "profiles", "LATEST")
 
 
-def measured_traffic(kernel_prefix, frames):
+def measured_traffic(kernel_prefix, frames, avg_ms=None):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary, or None
     when no summary exists for this batch size (PMC counters cannot be read inside the run)."""
     try:
@@ -42,6 +42,9 @@ def measured_traffic(kernel_prefix, frames):
         return None, tag
     for name, row in summ.items():
         if kernel_prefix in name and row.get("traffic_gb"):
+            # only valid for the kernel build that was profiled: its duration must agree
+            if avg_ms and abs(row["avg_ms"] - avg_ms) > 0.1 * avg_ms:
+                return None, tag + " (stale: profiled %.2f ms/launch)" % row["avg_ms"]
             return int(row["traffic_gb"] * 1e9), tag
     return None, tag
 
@@ -143,7 +146,7 @@ def main():
     avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     bytes_per_launch = intra_b / launches_per_step
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    traffic, prof_tag = measured_traffic("intra_rows_kernel", a.frames)
+    traffic, prof_tag = measured_traffic("intra_rows_kernel", a.frames, avg_launch_ms)
     out = {
         "metric": METRIC,
         "value": round(value, 1), "unit": "CTU/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,

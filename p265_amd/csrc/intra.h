@@ -25,12 +25,19 @@
 
 namespace p265r {
 
+// Intra job record written by intra_prep_kernel (layout: intra_prep.h).
+struct IntraJob {
+    uint32_t w[8];
+};
+
 struct DevPic {                 // per picture, device-resident table
     const p265r_ctu* ctus;
     const p265r_tb*  tbs;       // coef_off rewritten to pool offsets
     uint8_t* rec[3];            // pre-SAO planes (padded stride)
     uint8_t* out[3];            // SAO output planes (== rec when SAO is off)
     const uint8_t* nofilter;    // per 8x8 luma block or nullptr
+    IntraJob* jobs;             // same index space as tbs (jobs of a CTU start at tb_begin)
+    uint32_t* jcount;           // per CTU: number of jobs
 };
 
 struct Geo {                    // batch-uniform geometry

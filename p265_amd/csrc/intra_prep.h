@@ -1,0 +1,132 @@
+// Intra job preparation: everything about a transform block that does NOT depend on
+// reconstructed sample values, computed for all TBs of the batch in one fully parallel
+// pass, so that the serial per-CTU chain of intra_rows_kernel only moves samples.
+//
+// Per TB (decode order within its CTU) the pass derives
+//   * neighbour availability (6.4.1: picture edge, slice / tile of the neighbouring CTU,
+//     z-scan order inside the CTB - MinTbAddrZs, pps.py:246-262 / image.py:38-73) for
+//     every 4-luma-sample unit of the 4N+1 reference samples, as a bit mask in the
+//     linear order of 8.4.4.2.2 (bottom-left .. corner .. top-right);
+//   * the filtering decision of 8.4.4.2.3 (intraHorVerDistThres, strong-smoothing
+//     candidate), intraPredAngle and invAngle (Table 8-4/8-5);
+//   * where its residual lives (coefficient pool for bypass/PCM, residual pool else);
+// and pairs every Cb TB with the Cr TB of the same TU (4:2:0: same position, size and
+// mode, decoder/tu.py:127-135), so one wave reconstructs both with its two halves.
+// Replaces the per-sample tree walks of decoder/cu.py:617-632 and intra.py:82-136.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/p265r.h"
+#include "intra.h"
+#include "tables.h"
+
+namespace p265r {
+
+// 32-byte job record (w5..w7 reserved, 0).
+//  w0: [0,13) LDS offset of the TB origin in WaveLds (luma yr*64+xr, chroma 4096+yr*32+xr)
+//      [13,15) log2-2  [15,17) component mask (0 luma, 1 Cb, 2 Cr, 3 Cb+Cr)  [17,23) mode
+//      23 PCM  [24,26) filter (0 none, 1 [1 2 1], 2 strong candidate)
+//      [26,28) residual in the coefficient pool (bypass/PCM) per half
+//      [28,30) coded (residual non-zero) per half   30 all refs available   31 none available
+//  w1: [0,8) intraPredAngle (int8)  [8,21) -invAngle  21 availability bit 32
+//  w2: availability bits 0..31 (unit u: k in [u*us, u*us+us) for u < L, corner u = L,
+//      top units u > L; us = 4 luma / 2 chroma samples, L = 2N/us)
+//  w3, w4: residual element offset of half 0 (luma / Cb) and half 1 (Cr)
+// (struct IntraJob: intra.h)
+
+enum : uint32_t {
+    J_PCM = 1u << 23,
+    J_ALL = 1u << 30,
+    J_NONE = 1u << 31,
+};
+
+__device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265r_tb& cr) {
+    return cb.c_idx == 1 && cr.c_idx == 2 && cb.x == cr.x && cb.y == cr.y && cb.log2_size == cr.log2_size &&
+           cb.pred_mode == cr.pred_mode && ((cb.flags ^ cr.flags) & P265R_TB_PCM) == 0;
+}
+
+// grid (CTUs, pictures), 64 threads: one wave per CTU walks its TBs 64 at a time.
+__global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g) {
+    const DevPic P = pics[blockIdx.y];
+    const int addr = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int cx = addr % g.wc, cy = addr / g.wc;
+    const int ctb = 1 << g.ctb_log2;
+    const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
+    const p265r_ctu me = P.ctus[addr];
+    unsigned flags = 0;
+    if (cx > 0 && ctu_same_region(me, P.ctus[addr - 1])) flags |= 1u;
+    if (cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc])) flags |= 2u;
+    if (cx > 0 && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc - 1])) flags |= 4u;
+    if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc + 1])) flags |= 8u;
+
+    const p265r_tb* tbs = P.tbs + me.tb_begin;
+    IntraJob* jobs = P.jobs + me.tb_begin;
+    const int cnt = me.tb_count;
+    int out = 0;
+    for (int base = 0; base < cnt; base += 64) {
+        const int t = base + lane;
+        const bool valid = t < cnt;
+        p265r_tb rec{}, prev{}, next{};
+        if (valid) rec = tbs[t];
+        if (valid && t > 0) prev = tbs[t - 1];
+        if (valid && t + 1 < cnt) next = tbs[t + 1];
+        const bool cr_taken = valid && t > 0 && tb_same_tu_chroma(prev, rec);
+        const bool keep = valid && !cr_taken;
+        const unsigned long long km = __ballot(keep);
+        const int slot = out + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
+        out += __popcll(km);
+        if (keep) {
+            const int lg = rec.log2_size, n = 1 << lg, c = rec.c_idx;
+            const int sub = c ? 1 : 0;
+            const bool pair = c == 1 && t + 1 < cnt && tb_same_tu_chroma(rec, next);
+            const int xr = rec.x - (x0 >> sub), yr = rec.y - (y0 >> sub);
+            const uint32_t ofs = c == 0 ? (uint32_t)(yr * 64 + xr) : (uint32_t)(4096 + yr * 32 + xr);
+            const uint32_t cm = c == 0 ? 0u : (pair ? 3u : (uint32_t)c);
+            const int mode = rec.pred_mode;
+            // ---- availability per reference unit, linear order (8.4.4.2.2) -----------------
+            const int us_log = c ? 1 : 2;
+            const int L = (2 * n) >> us_log;
+            const int xc = xr << sub, yc = yr << sub;
+            unsigned long long m = 0;
+            for (int u = 0; u <= 2 * L; ++u) {
+                int dx, dy;
+                if (u < L) { dx = -1; dy = 2 * n - 1 - (u << us_log); }
+                else if (u == L) { dx = -1; dy = -1; }
+                else { dx = (u - L - 1) << us_log; dy = -1; }
+                if (nb_available_wh((xr + dx) << sub, (yr + dy) << sub, xc, yc, x0, y0, g.w, g.h, ctb, flags))
+                    m |= 1ull << u;
+            }
+            const unsigned long long full = (1ull << (2 * L + 1)) - 1ull;
+            // ---- filtering decision (8.4.4.2.3), luma only in 4:2:0 ---------------------------
+            uint32_t filt = 0;
+            if (c == 0 && n != 4 && mode != 1) {
+                const int dist = min(abs(mode - 26), abs(mode - 10));
+                if (dist > (n == 8 ? 7 : (n == 16 ? 1 : 0))) filt = (n == 32 && g.strong) ? 2u : 1u;
+            }
+            const uint32_t f0 = rec.flags;
+            const uint32_t f1 = pair ? next.flags : 0u;
+            // half 0 = luma / Cb, half 1 = Cr (an unpaired Cr TB lives in half 1)
+            const uint32_t fh0 = cm == 2 ? 0u : f0, fh1 = cm == 2 ? f0 : f1;
+            const uint32_t off0 = cm == 2 ? 0u : rec.coef_off, off1 = cm == 2 ? rec.coef_off : (pair ? next.coef_off : 0u);
+            auto raw = [](uint32_t f) { return (f & (P265R_TB_BYPASS | P265R_TB_PCM)) ? 1u : 0u; };
+            auto coded = [](uint32_t f) { return (f & (P265R_TB_CBF | P265R_TB_PCM)) ? 1u : 0u; };
+            IntraJob J;
+            J.w[0] = ofs | (uint32_t)(lg - 2) << 13 | cm << 15 | (uint32_t)mode << 17 |
+                     ((f0 & P265R_TB_PCM) ? J_PCM : 0u) | filt << 24 | raw(fh0) << 26 | raw(fh1) << 27 |
+                     coded(fh0) << 28 | coded(fh1) << 29 | (m == full ? J_ALL : 0u) | (m == 0 ? J_NONE : 0u);
+            J.w[1] = (uint32_t)(uint8_t)(int8_t)kIntraPredAngle[mode] | (uint32_t)(-kInvAngle[mode]) << 8 |
+                     (uint32_t)((m >> 32) & 1ull) << 21;
+            J.w[2] = (uint32_t)m;
+            J.w[3] = off0;
+            J.w[4] = off1;
+            J.w[5] = J.w[6] = J.w[7] = 0;
+            uint4* dst = reinterpret_cast<uint4*>(jobs + slot);
+            dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
+            dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
+        }
+    }
+    if (lane == 0) P.jcount[addr] = (uint32_t)out;
+}
+
+}  // namespace p265r

@@ -24,8 +24,7 @@
 #include <stdint.h>
 #include "../../include/p265r.h"
 #include "intra.h"
-
-extern "C" __device__ int __ockl_wfred_add_i32(int);
+#include "intra_prep.h"
 
 namespace p265r {
 
@@ -65,6 +64,11 @@ __device__ __forceinline__ T gload(const T* p) {
     return v;
 }
 
+// generic pointer to the LDS byte at 32-bit LDS address a
+__device__ __forceinline__ void* lds_ptr(uint32_t a) {
+    return (void*)(__attribute__((address_space(3))) void*)(uintptr_t)a;
+}
+
 struct WaveLds {                 // one wave's private CTU state (6816 B)
     uint8_t  y[64 * 64];         // interior luma, stride 64
     uint8_t  c[2][32 * 32];      // interior chroma, stride 32
@@ -90,58 +94,62 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// index of the value that substitutes linear entry k (8.4.4.2.2), given the
-// availability masks of entries 0..63, 64..127, 128 (m0, m1, m2).  -1: none available.
-__device__ __forceinline__ int subst_src(int k, unsigned long long m0, unsigned long long m1,
-                                         unsigned long long m2) {
-    const int j = k >> 6, b = k & 63;
-    const unsigned long long mj = j == 0 ? m0 : (j == 1 ? m1 : m2);
-    if ((mj >> b) & 1ull) return k;
-    const unsigned long long below = b ? (mj & ((1ull << b) - 1ull)) : 0ull;
-    if (below) return 64 * j + 63 - __clzll((long long)below);
-    if (j >= 2 && m1) return 64 + 63 - __clzll((long long)m1);
-    if (j >= 1 && m0) return 63 - __clzll((long long)m0);
-    if (m0) return __ffsll((long long)m0) - 1;
-    if (m1) return 64 + __ffsll((long long)m1) - 1;
-    if (m2) return 128 + __ffsll((long long)m2) - 1;
-    return -1;
-}
-
-struct CtuCtx {                  // wave-uniform state of the CTU being reconstructed
-    int x0, y0, w, h, cw, ctb;
-    unsigned flags;              // bit0 L, bit1 T, bit2 TL, bit3 TR available
-    int bd_l, bd_c, strong;
-};
-
 __device__ __forceinline__ int clip_pel(int v, int maxv) { return min(max(v, 0), maxv); }
 
-// Reconstruct one TB of size 2^LOG2.  tw1 = TB record word 1 (log2 | c | mode | flags),
-// (tx, ty) its position; (ra, rb) this lane's residual words (prefetched).
-template <int LOG2>
-__device__ __forceinline__ void recon_tb(const CtuCtx& X, WaveLds& L, const uint8_t* line_up,
-                                        int tx, int ty, int c, int mode, int flags,
-                                        uint4 ra, uint4 rb, int lane) {
+// sum of v over the 32-lane half of the wave (PAIR) or the whole wave
+template <bool PAIR>
+__device__ __forceinline__ int wave_sum(int v, int half) {
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);   // row_half_mirror
+    v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true);   // row_mirror: every lane holds its row's sum
+    const int s0 = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);
+    const int s1 = __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+    return PAIR ? (half ? s1 : s0) : s0 + s1;
+}
+
+// Reconstruct one intra job of size 2^LOG2: a luma TB (PAIR = false, 64 lanes) or the
+// Cb/Cr TBs of one TU (PAIR = true, lanes 0-31 Cb, 32-63 Cr).  (w0, w1, w2) = job words
+// (intra_prep.h), (ra, rb) = this lane's prefetched residual chunks, line_top = the
+// row above the CTU for this lane's component, at the CTU's first column.
+//
+// Reference samples (8.4.4.2.2) are gathered straight from the LDS copies of the
+// neighbourhood (CTU interior, left column, line buffer), every lane reading the sample
+// that substitutes its entry (availability comes precomputed per 4-luma-sample unit),
+// so substitution costs no extra round trip; luma filtering (8.4.4.2.3) adds one.
+template <int LOG2, bool PAIR>
+__device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
+                                          uint32_t w2, uint4 ra, uint4 rb, int lane) {
     constexpr int n = 1 << LOG2;
     constexpr int nn = n * n;
-    constexpr int S = nn >= 64 ? nn / 64 : 1;        // samples per lane (raster run)
+    constexpr int LANES = PAIR ? 32 : 64;
+    constexpr int S = nn >= LANES ? nn / LANES : 1;       // samples per lane (raster run)
     constexpr int nref = 4 * n + 1;
-    constexpr int NCH = (nref + 63) / 64;
-    const int sub = c ? 1 : 0;
-    const int xr = tx - (X.x0 >> sub), yr = ty - (X.y0 >> sub);
-    const int bd = c ? X.bd_c : X.bd_l;
-    const int maxv = (1 << bd) - 1;
-    uint8_t* interior = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
-    const int ist = c ? 32 : 64;
-    const uint8_t* top = line_up + (c == 0 ? 0 : (c == 1 ? X.w : X.w + X.cw)) + (X.x0 >> sub);
-    const uint8_t* left = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
-    const bool own = lane * S < nn;
-    const int sidx = own ? lane * S : 0;
+    constexpr int NCH = (nref + LANES - 1) / LANES;
+    constexpr int US = PAIR ? 1 : 2;                      // log2 availability unit (samples)
+    constexpr int NU = (2 * n) >> US;                     // units per side
+    constexpr int maxv = 255;                             // 8-bit samples (P265R_EUNSUPPORTED otherwise)
+    const int hl = PAIR ? (lane & 31) : lane;
+    const int half = PAIR ? (lane >> 5) : 0;
+    const int ofs = (int)(w0 & 0x1fffu);
+    const int xr = PAIR ? ((ofs - 4096) & 31) : (ofs & 63);
+    const int yr = PAIR ? ((ofs - 4096) >> 5) : (ofs >> 6);
+    constexpr int ist = PAIR ? 32 : 64;
+    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + ofs + half * 1024;     // TB origin in the interior
+    const uint8_t* const lcol = (PAIR ? L.cleft[half] : L.yleft) + yr;
+    const int mode = (int)((w0 >> 17) & 63u);
+    const bool own = hl * S < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
+    const int sidx = hl * S < nn ? hl * S : 0;
     const int sy = sidx >> LOG2, sx = sidx & (n - 1);
-    // (ra, rb): the two aligned 16-B chunks holding this lane's residual run (see res_addr)
+    const bool coded = (w0 >> (28 + half)) & 1u;
+    if (!coded) { ra = make_uint4(0, 0, 0, 0); rb = ra; }
     uint32_t rw[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
     if constexpr (S == 4) {
         const bool hi = sidx & 4;
         rw[0] = hi ? ra.z : ra.x; rw[1] = hi ? ra.w : ra.y;
+    } else if constexpr (S == 2) {
+        const int e = (sidx & 7) >> 1;
+        rw[0] = e == 0 ? ra.x : (e == 1 ? ra.y : (e == 2 ? ra.z : ra.w));
     } else if constexpr (S == 1) {
         const int e = sidx & 7;
         const uint32_t wd = e < 2 ? ra.x : (e < 4 ? ra.y : (e < 6 ? ra.z : ra.w));
@@ -153,79 +161,76 @@ __device__ __forceinline__ void recon_tb(const CtuCtx& X, WaveLds& L, const uint
     for (int q = 0; q < (S + 3) / 4; ++q) outw[q] = 0;
     auto put = [&](int i, int v) { outw[i >> 2] |= (uint32_t)clip_pel(v + resv(i), maxv) << (8 * (i & 3)); };
 
-    if (flags & P265R_TB_PCM) {
+    if (w0 & J_PCM) {
 #pragma unroll
         for (int i = 0; i < S; ++i) put(i, 0);
     } else {
-        // ---- A: gather raw reference samples + availability (6.4.1) --------------------
-        const int xcl = xr << sub, ycl = yr << sub;
-        unsigned long long m[3] = {0ull, 0ull, 0ull};
+        // ---- gather (+ substitution) --------------------------------------------------
+        const int filt = PAIR ? 0 : (int)((w0 >> 24) & 3u);
+        uint16_t* const R0 = PAIR ? L.ref[half] : L.ref[0];
+        uint16_t* const RF = (PAIR || !filt) ? R0 : L.ref[1];
+        // sources: left column (entries 0..2n-1), corner (2n), top row (2n+1..4n)
+        const uint8_t* const lbase = xr == 0 ? lcol : org - 1;
+        const int lstep = xr == 0 ? 1 : ist;
+        const uint8_t* const tbase = yr == 0 ? line_top + xr : org - ist;
+        const uint8_t* const cptr = yr == 0 ? line_top + xr - 1 : (xr == 0 ? lcol - 1 : org - ist - 1);
+        const unsigned long long m = (unsigned long long)w2 | ((unsigned long long)((w1 >> 21) & 1u) << 32);
+        const bool all = w0 & J_ALL, none = w0 & J_NONE;
+        int dcs = 0;
 #pragma unroll
         for (int jj = 0; jj < NCH; ++jj) {
-            const int k = lane + 64 * jj;
-            bool av = false;
-            if (k < nref) {
-                const int dx = k <= 2 * n ? -1 : k - 2 * n - 1;
-                const int dy = k < 2 * n ? 2 * n - 1 - k : -1;
-                const int xn = xr + dx, yn = yr + dy;
-                av = nb_available_wh(xn << sub, yn << sub, xcl, ycl, X.x0, X.y0, X.w, X.h, X.ctb, X.flags);
-                int v = 0;
-                if (av) v = yn < 0 ? top[xn] : (xn < 0 ? left[yn] : interior[yn * ist + xn]);
-                L.ref[0][k] = (uint16_t)v;
+            const int k = hl + LANES * jj;
+            if (jj + 1 < NCH || k < nref) {
+                int s = k;
+                if (!all) {
+                    const int u = k < 2 * n ? (k >> US) : (k == 2 * n ? NU : NU + 1 + ((k - 2 * n - 1) >> US));
+                    const unsigned long long below = m & ((1ull << u) - 1ull);
+                    if (!((m >> u) & 1ull)) {
+                        if (below) {
+                            const int ub = 63 - __clzll((long long)below);        // nearest available unit below
+                            s = ub < NU ? (ub << US) + (1 << US) - 1 : (ub == NU ? 2 * n : 2 * n + ((ub - NU) << US));
+                        } else {
+                            const int uf = __ffsll((long long)m) - 1;             // first available unit
+                            s = uf < NU ? (uf << US) : (uf == NU ? 2 * n : 2 * n + 1 + ((uf - NU - 1) << US));
+                        }
+                    }
+                }
+                const uint8_t* src = s < 2 * n ? lbase + (2 * n - 1 - s) * lstep : (s == 2 * n ? cptr : tbase + (s - 2 * n - 1));
+                const int v = none ? 128 : (int)*src;
+                R0[k] = (uint16_t)v;
+                if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) dcs += v;
             }
-            m[jj] = __ballot(av);
-        }
-        constexpr unsigned long long full0 = nref >= 64 ? ~0ull : ((1ull << (nref & 63)) - 1ull);
-        constexpr unsigned long long full1 = nref >= 128 ? ~0ull : (nref > 64 ? ((1ull << ((nref - 64) & 63)) - 1ull) : 0ull);
-        constexpr unsigned long long full2 = nref > 128 ? 1ull : 0ull;
-        const bool all = m[0] == full0 && m[1] == full1 && m[2] == full2;
-        bool filt = false;
-        if (n != 4 && c == 0 && mode != 1) {
-            const int dist = min(abs(mode - 26), abs(mode - 10));
-            filt = dist > (n == 8 ? 7 : (n == 16 ? 1 : 0));
         }
         wave_sync();
-        const uint16_t* R = L.ref[0];
-        int dcs = 0;
-        if (!all || filt || mode == 1) {
-            // ---- B: substitution (8.4.4.2.2) + filtering (8.4.4.2.3) -> ref[1] ------------
-            const bool any = (m[0] | m[1] | m[2]) != 0ull;
-            const int half = 1 << (bd - 1);
-            auto sval = [&](int i) -> int {
-                if (all) return (int)L.ref[0][i];
-                const int s = subst_src(i, m[0], m[1], m[2]);
-                return s < 0 ? half : (int)L.ref[0][s];
-            };
+        if (!PAIR && filt) {
+            // ---- filtering (8.4.4.2.3): [1 2 1], or strong bi-linear for 32x32 -----------
             bool strong = false;
             int corner = 0, bl = 0, tr = 0;
-            if (n == 32 && filt && X.strong) {
-                corner = sval(2 * n); bl = sval(0); tr = sval(4 * n);
-                strong = abs(corner + tr - 2 * sval(3 * n)) < (1 << (bd - 5)) &&
-                         abs(corner + bl - 2 * sval(n)) < (1 << (bd - 5));
+            if (n == 32 && filt == 2) {
+                corner = R0[2 * n]; bl = R0[0]; tr = R0[4 * n];
+                strong = abs(corner + tr - 2 * (int)R0[3 * n]) < 8 && abs(corner + bl - 2 * (int)R0[n]) < 8;
             }
 #pragma unroll
             for (int jj = 0; jj < NCH; ++jj) {
                 const int k = lane + 64 * jj;
-                if (k < nref) {
-                    const int sk = any ? sval(k) : half;
-                    int f = sk;
-                    if (filt && k > 0 && k < 4 * n) {
+                if (jj + 1 < NCH || k < nref) {
+                    int f = R0[k];
+                    if (k > 0 && k < 4 * n) {
                         if (strong) {
                             f = k == 2 * n ? corner
                               : (k < 2 * n ? ((63 - (2 * n - 1 - k)) * corner + (2 * n - k) * bl + 32) >> 6
                                            : ((63 - (k - 2 * n - 1)) * corner + (k - 2 * n) * tr + 32) >> 6);
                         } else {
-                            f = (sval(k - 1) + 2 * sk + sval(k + 1) + 2) >> 2;
+                            f = ((int)R0[k - 1] + 2 * f + (int)R0[k + 1] + 2) >> 2;
                         }
                     }
-                    L.ref[1][k] = (uint16_t)f;
-                    if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) dcs += sk;
+                    RF[k] = (uint16_t)f;
                 }
             }
             wave_sync();
-            R = L.ref[1];
         }
-        // ---- C: prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ----------------
+        const uint16_t* const R = RF;
+        // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------
         if (mode == 0) {
             const int trs = R[3 * n + 1], bls = R[n - 1];
             const int ly = R[2 * n - 1 - sy];
@@ -235,8 +240,8 @@ __device__ __forceinline__ void recon_tb(const CtuCtx& X, WaveLds& L, const uint
                 put(i, ((n - 1 - x) * ly + (x + 1) * trs + (n - 1 - sy) * R[2 * n + 1 + x] + (sy + 1) * bls + n) >> (LOG2 + 1));
             }
         } else if (mode == 1) {
-            const int dc = (__ockl_wfred_add_i32(dcs) + n) >> (LOG2 + 1);
-            const bool edge = c == 0 && n < 32;
+            const int dc = (wave_sum<PAIR>(dcs, half) + n) >> (LOG2 + 1);
+            constexpr bool edge = !PAIR && n < 32;
 #pragma unroll
             for (int i = 0; i < S; ++i) {
                 const int x = sx + i;
@@ -248,42 +253,44 @@ __device__ __forceinline__ void recon_tb(const CtuCtx& X, WaveLds& L, const uint
                 }
                 put(i, v);
             }
-        } else if (mode >= 18) {                                    // vertical family
-            const int ang = c_angle[mode];
-            const int inv = c_inv_angle[mode];
-            const int idx = ((sy + 1) * ang) >> 5, fact = ((sy + 1) * ang) & 31;
-            auto refk = [&](int r) { return r >= 0 ? 2 * n + r : 2 * n - ((r * inv + 128) >> 8); };
-            const bool bflt = mode == 26 && c == 0 && n < 32;
+        } else {
+            const int ang = (int)(int8_t)(w1 & 0xffu);
+            const int inv = -(int)((w1 >> 8) & 0x1fffu);
+            if (mode >= 18) {                                        // vertical family
+                const int idx = ((sy + 1) * ang) >> 5, fact = ((sy + 1) * ang) & 31;
+                auto refk = [&](int r) { return r >= 0 ? 2 * n + r : 2 * n - ((r * inv + 128) >> 8); };
+                const bool bflt = !PAIR && n < 32 && mode == 26;
 #pragma unroll
-            for (int i = 0; i < S; ++i) {
-                const int x = sx + i;
-                const int r0 = x + idx + 1;
-                int v = R[refk(r0)];
-                if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
-                if (bflt && x == 0) v = clip_pel((int)R[2 * n + 1] + (((int)R[2 * n - 1 - sy] - (int)R[2 * n]) >> 1), maxv);
-                put(i, v);
-            }
-        } else {                                                    // horizontal family
-            const int ang = c_angle[mode];
-            const int inv = c_inv_angle[mode];
-            auto refk = [&](int r) { return r >= 0 ? 2 * n - r : 2 * n + ((r * inv + 128) >> 8); };
-            const bool bflt = mode == 10 && c == 0 && n < 32 && sy == 0;
+                for (int i = 0; i < S; ++i) {
+                    const int x = sx + i;
+                    const int r0 = x + idx + 1;
+                    int v = R[refk(r0)];
+                    if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
+                    if (bflt && x == 0) v = clip_pel((int)R[2 * n + 1] + (((int)R[2 * n - 1 - sy] - (int)R[2 * n]) >> 1), maxv);
+                    put(i, v);
+                }
+            } else {                                                 // horizontal family
+                auto refk = [&](int r) { return r >= 0 ? 2 * n - r : 2 * n + ((r * inv + 128) >> 8); };
+                const bool bflt = !PAIR && n < 32 && mode == 10 && sy == 0;
 #pragma unroll
-            for (int i = 0; i < S; ++i) {
-                const int x = sx + i;
-                const int idx = ((x + 1) * ang) >> 5, fact = ((x + 1) * ang) & 31;
-                const int r0 = sy + idx + 1;
-                int v = R[refk(r0)];
-                if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
-                if (bflt) v = clip_pel((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), maxv);
-                put(i, v);
+                for (int i = 0; i < S; ++i) {
+                    const int x = sx + i;
+                    const int idx = ((x + 1) * ang) >> 5, fact = ((x + 1) * ang) & 31;
+                    const int r0 = sy + idx + 1;
+                    int v = R[refk(r0)];
+                    if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
+                    if (bflt) v = clip_pel((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), maxv);
+                    put(i, v);
+                }
             }
         }
     }
     if (own) {
-        uint8_t* dst = interior + (yr + sy) * ist + xr + sx;
+        uint8_t* dst = org + sy * ist + sx;
         if constexpr (S == 16) *reinterpret_cast<uint4*>(dst) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+        else if constexpr (S == 8) *reinterpret_cast<uint2*>(dst) = make_uint2(outw[0], outw[1]);
         else if constexpr (S == 4) *reinterpret_cast<uint32_t*>(dst) = outw[0];
+        else if constexpr (S == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)outw[0];
         else dst[0] = (uint8_t)outw[0];
     }
     wave_sync();
@@ -351,7 +358,10 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         P265R_TRACE(2 | (r << 8));
         const int j = r / g.hc, cy = r - j * g.hc;
         const int slot = j % fs_count, gen = j / fs_count;
-        const DevPic P = uniform(gload(pics + b + j * G));
+        const DevPic* Pp = pics + b + j * G;
+        const p265r_ctu* ctus = uniform(gload(&Pp->ctus));
+        const IntraJob* jobs = uniform(gload(&Pp->jobs));
+        const uint32_t* jcount = uniform(gload(&Pp->jcount));
         // picture slot reuse: every row of picture j waits until picture j - fs_count (the
         // slot's previous occupant) has completed all its rows; those rows were dequeued
         // earlier and are held by running waves, so this wait always ends.
@@ -365,7 +375,6 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         const int* up_prog = &prog[slot * g.hc + (cy > 0 ? cy - 1 : 0)];
         const int tag = (j & 0xffff) << 16;
         __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const p265r_ctu* ctus = P.ctus;
 
         for (int cx = 0; cx < g.wc; ++cx) {
             // ---- wait for the row above (2-CTU lag) -------------------------------------
@@ -377,75 +386,76 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                     })) { failed = true; break; }
             }
             P265R_TRACE(4 | (cx << 8) | (r << 16));
-            CtuCtx X;
-            X.x0 = cx << g.ctb_log2; X.y0 = cy << g.ctb_log2;
-            X.w = g.w; X.h = g.h; X.cw = g.cw; X.ctb = ctb;
-            X.bd_l = g.bd[0]; X.bd_c = g.bd[1]; X.strong = g.strong;
+            const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
             const int addr = cy * g.wc + cx;
-            // the CTU and its four causal neighbours: five independent loads, one wait
-            const p265r_ctu me = uniform(gload(ctus + addr));
-            const p265r_ctu nl = uniform(gload(ctus + (cx > 0 ? addr - 1 : addr)));
-            const p265r_ctu nt_ = uniform(gload(ctus + (cy > 0 ? addr - g.wc : addr)));
-            const p265r_ctu ntl = uniform(gload(ctus + (cx > 0 && cy > 0 ? addr - g.wc - 1 : addr)));
-            const p265r_ctu ntr = uniform(gload(ctus + (cx + 1 < g.wc && cy > 0 ? addr - g.wc + 1 : addr)));
-            unsigned flags = 0;
-            if (cx > 0 && ctu_same_region(me, nl)) flags |= 1u;
-            if (cy > 0 && ctu_same_region(me, nt_)) flags |= 2u;
-            if (cx > 0 && cy > 0 && ctu_same_region(me, ntl)) flags |= 4u;
-            if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, ntr)) flags |= 8u;
-            X.flags = flags;
+            // this CTU's job list (intra_prep_kernel): first job = its first TB index
+            const uint32_t tb_begin = uniform(gload(reinterpret_cast<const uint2*>(ctus + addr))).x;
+            const int nt = (int)__builtin_amdgcn_readfirstlane(*gptr(jcount + addr));
+            const IntraJob* jl = jobs + tb_begin;
+            uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
+            if (lane < nt) { rec0 = ld16(&jl[lane].w[0]); rec1 = ld16(&jl[lane].w[4]); }
+            // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr)
+            const uint8_t* ltop_l = line_up + x0;
+            const uint8_t* ltop_c = line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
 
-            const int nt = me.tb_count;
-            const uint4* trec = reinterpret_cast<const uint4*>(P.tbs + me.tb_begin);
-            uint4 rec = make_uint4(0, 0, 0, 0);
-            if (lane < nt) rec = ld16(trec + lane);
-
-            // residual of TB t: always two aligned 16-B loads per lane (fixed shape, so the
-            // compiler's vmcnt bookkeeping stays exact; pools are padded by 64 B), issued
-            // while TB t-1 is processed.  TB offsets are multiples of 16 elements.
-            auto res_addr = [&](uint32_t w1, uint32_t off) {
-                const int lg = (int)(w1 & 0xff), fl = (int)(w1 >> 24);
-                const int nn = 1 << (2 * lg);
-                const int S = nn >= 64 ? (nn >> 6) : 1;
-                const int sidx = lane * S < nn ? lane * S : 0;
-                const int16_t* base = (fl & (P265R_TB_BYPASS | P265R_TB_PCM)) ? pool : resid;
-                return reinterpret_cast<const uint4*>(base + off + (sidx & ~7));
+            // residual of job t: two aligned 16-B loads per lane (fixed shape, pools padded
+            // by 64 B), issued while job t-1 is processed.  TB offsets are multiples of 16.
+            auto res_addr = [&](uint32_t w0, uint32_t w3, uint32_t w4) {
+                const int lg = (int)((w0 >> 13) & 3u) + 2;
+                const bool pr = (w0 >> 15) & 3u;
+                const int h = pr ? (lane >> 5) : 0;
+                const int hl = pr ? (lane & 31) : lane;
+                const int ls = 2 * lg - (pr ? 5 : 6);
+                const int S = ls > 0 ? (1 << ls) : 1;
+                const int sidx = hl * S < (1 << (2 * lg)) ? hl * S : 0;
+                const int16_t* base = ((w0 >> (26 + h)) & 1u) ? pool : resid;
+                return reinterpret_cast<const uint4*>(base + (h ? w4 : w3) + (sidx & ~7));
             };
-            uint32_t w0n = 0, w1n = 0, w3n = 0;
+            uint32_t w0n = 0, w1n = 0, w2n = 0;
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
             if (nt) {
-                w0n = __builtin_amdgcn_readlane(rec.x, 0);
-                w1n = __builtin_amdgcn_readlane(rec.y, 0);
-                w3n = __builtin_amdgcn_readlane(rec.w, 0);
-                const uint4* a = res_addr(w1n, w3n);
+                w0n = __builtin_amdgcn_readlane(rec0.x, 0);
+                w1n = __builtin_amdgcn_readlane(rec0.y, 0);
+                w2n = __builtin_amdgcn_readlane(rec0.z, 0);
+                const uint4* a = res_addr(w0n, __builtin_amdgcn_readlane(rec0.w, 0), __builtin_amdgcn_readlane(rec1.x, 0));
                 ra = ld16(a); rb = ld16(a + 1);
             }
             for (int t = 0; t < nt; ++t) {
-                const uint32_t w0 = w0n, w1 = w1n;
+                const uint32_t w0 = w0n, w1 = w1n, w2 = w2n;
                 const uint4 ca = ra, cb = rb;
-                const bool coded = (w1 >> 24) & (P265R_TB_CBF | P265R_TB_PCM);
                 if (t + 1 < nt) {
                     const int l = (t + 1) & 63;
                     if (l == 0) {
-                        if (t + 1 + lane < nt) rec = ld16(trec + t + 1 + lane);
-                        else rec = make_uint4(0, 0, 0, 0);
+                        if (t + 1 + lane < nt) { rec0 = ld16(&jl[t + 1 + lane].w[0]); rec1 = ld16(&jl[t + 1 + lane].w[4]); }
+                        else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
                     }
-                    w0n = __builtin_amdgcn_readlane(rec.x, l);
-                    w1n = __builtin_amdgcn_readlane(rec.y, l);
-                    w3n = __builtin_amdgcn_readlane(rec.w, l);
-                    const uint4* a = res_addr(w1n, w3n);
+                    w0n = __builtin_amdgcn_readlane(rec0.x, l);
+                    w1n = __builtin_amdgcn_readlane(rec0.y, l);
+                    w2n = __builtin_amdgcn_readlane(rec0.z, l);
+                    const uint4* a = res_addr(w0n, __builtin_amdgcn_readlane(rec0.w, l), __builtin_amdgcn_readlane(rec1.x, l));
                     ra = ld16(a); rb = ld16(a + 1);
                 }
-                const uint4 za = coded ? ca : make_uint4(0, 0, 0, 0);
-                const uint4 zb = coded ? cb : make_uint4(0, 0, 0, 0);
-                const int tx = (int)(w0 & 0xffff), ty = (int)(w0 >> 16);
-                const int lg = (int)(w1 & 0xff), c = (int)((w1 >> 8) & 0xff);
-                const int mode = (int)((w1 >> 16) & 0xff), fl = (int)(w1 >> 24);
-                switch (lg) {
-                    case 2: recon_tb<2>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
-                    case 3: recon_tb<3>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
-                    case 4: recon_tb<4>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
-                    default: recon_tb<5>(X, L, line_up, tx, ty, c, mode, fl, za, zb, lane); break;
+                const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
+                // Opaque copies of the lane id and the LDS bases: keeps the compiler from
+                // hoisting every template's lane-derived constants out of the job loop
+                // (7 inlined instances would otherwise hold them all live: ~150 VGPRs).
+                int ln;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+                uint32_t lbase, tl, tc;
+                asm volatile("s_mov_b32 %0, %1" : "=s"(lbase) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&L)));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"((uint32_t)(uintptr_t)ltop_l));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(tc) : "v"((uint32_t)(uintptr_t)ltop_c));
+                WaveLds& LL = *reinterpret_cast<WaveLds*>(lds_ptr(lbase));
+                const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
+                const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
+                switch (sel) {
+                    case 0: recon_job<2, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
+                    case 1: recon_job<3, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
+                    case 2: recon_job<4, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
+                    case 3: recon_job<5, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
+                    case 4: recon_job<2, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
+                    case 5: recon_job<3, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
+                    default: recon_job<4, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
                 }
             }
 
@@ -456,11 +466,11 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const int sub = c ? 1 : 0;
                 const int cs = ctb >> sub;
                 const int Wd = c ? g.cw : g.w, Ht = c ? g.ch : g.h;
-                const int xb = X.x0 >> sub, yb = X.y0 >> sub;
+                const int xb = x0 >> sub, yb = y0 >> sub;
                 const int wv = min(cs, Wd - xb), hv = min(cs, Ht - yb);
                 const uint8_t* src = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
                 const int ist = c ? 32 : 64;
-                P265R_GLOBAL uint8_t* plane = gptr_w(P.rec[c]);
+                P265R_GLOBAL uint8_t* plane = gptr_w(uniform(gload(&Pp->rec[c])));
                 const int st = g.stride[c];
                 const int gpr = wv >> 2;
                 for (int e = lane; e < gpr * hv; e += 64) {

@@ -19,6 +19,7 @@
 
 #include "../../include/p265r.h"
 #include "intra.h"
+#include "intra_prep.h"
 #include "intra_rows.h"
 #include "residual.h"
 #include "sao.h"
@@ -321,6 +322,9 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t o_res = off; off = align_up(off + sizeof(int16_t) * pool_total + 64, 256);
     size_t o_jobs[RC_NUM];
     for (int c = 0; c < RC_NUM; ++c) { o_jobs[c] = off; off = align_up(off + sizeof(ResJob) * n_jobs[c], 256); }
+    // intra jobs (same index space as the TB records) + per-CTU job counts
+    const size_t o_ijobs = off; off = align_up(off + sizeof(IntraJob) * n_tbs_total, 256);
+    const size_t o_jcount = off; off = align_up(off + sizeof(uint32_t) * nc * (size_t)n_pics, 256);
     size_t o_nf = off;
     size_t nf_bytes = (size_t)g.nf_w * ((g.h + 7) / 8);
     size_t n_nf = 0;
@@ -377,6 +381,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         DevPic& dp = b->h_pics[i];
         dp.ctus = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus) + (size_t)i * nc;
         dp.tbs = reinterpret_cast<const p265r_tb*>(dbase + o_tbs) + tb_fill;
+        dp.jobs = reinterpret_cast<IntraJob*>(dbase + o_ijobs) + tb_fill;
+        dp.jcount = reinterpret_cast<uint32_t*>(dbase + o_jcount) + (size_t)i * nc;
         unsigned char* rec = dbase + o_rec + pic_plane_bytes * i;
         dp.rec[0] = rec;
         dp.rec[1] = rec + align_up(plane_bytes[0], 256);
@@ -436,6 +442,12 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     if (b->n_jobs[RC_TSKIP]) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
+        ++tm.residual_launches;
+    }
+    if (ctx->schedule == 1) {
+        // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
+        // of the residuals, timed with the residual phase
+        intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
         ++tm.residual_launches;
     }
     HIP_TRY(hipGetLastError());
