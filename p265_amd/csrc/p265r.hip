@@ -475,7 +475,14 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // ---- SAO -----------------------------------------------------------------------
     if (b->sao) {
-        sao_kernel<<<dim3(ctx->n_ctus, b->n_pics), 256, 0, s>>>(b->d_pics, g);
+        const int cs = 1 << g.ctb_log2;
+        if (g.ctb_log2 >= 5) {
+            const int threads = (cs / 16) * cs + 2 * (cs / 32) * (cs / 2);
+            sao_kernel<16><<<dim3(ctx->n_ctus, b->n_pics), (threads + 63) / 64 * 64, 0, s>>>(b->d_pics, g);
+        } else {
+            const int threads = (cs / 8) * cs + 2 * (cs / 16) * (cs / 2);
+            sao_kernel<8><<<dim3(ctx->n_ctus, b->n_pics), (threads + 63) / 64 * 64, 0, s>>>(b->d_pics, g);
+        }
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
     }

@@ -164,3 +164,24 @@ def test_many_small_pictures_per_workgroup(recon_mod, schedule):
     for i in range(len(pics)):
         for c in range(3):
             np.testing.assert_array_equal(outs[i][c], refs[i % 5][c], err_msg="pic %d c%d" % (i, c))
+
+
+def _component_major(pic):
+    """Same picture with each CTU's TBs reordered to [all Y, all Cb, all Cr]: the decode
+    order inside every component is unchanged, so the output must be identical; the Cb
+    and Cr TBs of a TU are no longer adjacent (unpaired chroma jobs)."""
+    tbs = pic.tbs.copy()
+    for ctu in pic.ctus:
+        b, n = int(ctu["tb_begin"]), int(ctu["tb_count"])
+        seg = pic.tbs[b:b + n]
+        order = np.argsort(seg["c_idx"], kind="stable")
+        tbs[b:b + n] = seg[order]
+    return R.Picture(ctus=pic.ctus, tbs=tbs, coef=pic.coef, nofilter=pic.nofilter, meta=dict(pic.meta))
+
+
+def test_component_major_tb_order(recon_mod):
+    params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5)
+    pics = [_component_major(synth.make_picture(params, 4040 + s, perf=False)) for s in range(2)]
+    _check(recon_mod, params, pics, "component-major")
+    params, sp = frontend.pictures_from_frontend_npz(os.path.join(GOLDEN, "sanity_frontend.npz"))
+    _check(recon_mod, params, [_component_major(sp[0])], "sanity-component-major")
