@@ -52,9 +52,16 @@ extern "C" {
 
 /* p265r_ctu.flags */
 #define P265R_CTU_LF_ACROSS_SLICES 0x01u  /* slice_loop_filter_across_slices_enabled_flag of its slice */
+#define P265R_CTU_DEBLOCK          0x02u  /* deblocking on in its slice (!slice_deblocking_filter_disabled_flag,
+                                             slice.py:170-175 / pps.py:122-131); 0 = the edges this CTU's
+                                             coding blocks own (left/top/internal) are not filtered     */
+
+/* p265r_ctu.deblock_offsets: slice_beta_offset_div2 in bits 0..3, slice_tc_offset_div2 in bits
+ * 4..7, each a 4-bit two's-complement value in -6..6 (inherited from pps_*_offset_div2) */
+#define P265R_DEBLOCK_OFFSETS(beta_div2, tc_div2) ((uint8_t)(((beta_div2) & 15) | (((tc_div2) & 15) << 4)))
 
 /* Sequence-level parameters (SPS/PPS-derived fields the path reads; sps.py:59-62,
- * sps.py:142-171, sps.py:120, pps.py:38).  POD, 32 bytes: RCCL-broadcastable. */
+ * sps.py:142-171, sps.py:120, pps.py:38, pps.py:49-50).  POD, 32 bytes: RCCL-broadcastable. */
 typedef struct p265r_params {
     uint32_t version;                 /* = P265R_ABI_VERSION                      */
     uint16_t pic_width;               /* pic_width_in_luma_samples                */
@@ -70,7 +77,9 @@ typedef struct p265r_params {
     uint8_t  sample_adaptive_offset;  /* sample_adaptive_offset_enabled_flag      */
     uint8_t  loop_filter_across_tiles;/* loop_filter_across_tiles_enabled_flag    */
     uint8_t  scaling_list_enabled;    /* must be 0 in this version                */
-    uint8_t  reserved[13];
+    int8_t   pps_cb_qp_offset;        /* cQpPicOffset of Cb chroma deblocking (8.7.2.5.5) */
+    int8_t   pps_cr_qp_offset;        /* cQpPicOffset of Cr chroma deblocking     */
+    uint8_t  reserved[11];
 } p265r_params;
 
 /* One CTU, raster order, PicSizeInCtbsY per picture.  32 bytes. */
@@ -82,7 +91,7 @@ typedef struct p265r_ctu {
     uint8_t  flags;           /* P265R_CTU_*                                                   */
     uint8_t  sao_type[3];     /* SaoTypeIdx[cIdx]: 0 off, 1 band offset, 2 edge offset         */
     uint8_t  sao_class[3];    /* sao_band_position (type 1) or SaoEoClass (type 2)             */
-    uint8_t  reserved;
+    uint8_t  deblock_offsets; /* P265R_DEBLOCK_OFFSETS(slice_beta_offset_div2, slice_tc_offset_div2) */
     int8_t   sao_offset[3][4];/* SaoOffsetVal[cIdx][1..4]: signed, << log2OffsetScale          */
 } p265r_ctu;
 
@@ -95,7 +104,8 @@ typedef struct p265r_tb {
     uint8_t  c_idx;           /* 0 Y, 1 Cb, 2 Cr                                               */
     uint8_t  pred_mode;       /* IntraPredModeY / IntraPredModeC, 0..34                        */
     uint8_t  flags;           /* P265R_TB_*                                                    */
-    uint8_t  qp;              /* qP for scaling: Qp'Y or Qp'Cb / Qp'Cr (incl. QpBdOffset)      */
+    uint8_t  qp;              /* qP for scaling: Qp'Y or Qp'Cb / Qp'Cr (incl. QpBdOffset); luma
+                                 TBs (PCM ones too) also give QpY + QpBdOffsetY to deblocking    */
     uint8_t  reserved[3];
     uint32_t coef_off;        /* int16 offset of the N*N TransCoeffLevel[y][x] (iff CBF|PCM)   */
 } p265r_tb;
@@ -109,11 +119,12 @@ typedef struct p265r_picture {
     const int16_t*   coef;
     uint64_t         n_coef;
     const uint8_t*   nofilter;/* optional (NULL): per 8x8 luma block, raster, ceil(W/8) wide;
-                                 1 = SAO leaves the block's samples untouched
+                                 1 = deblocking and SAO leave the block's samples untouched
                                  (pcm_loop_filter_disabled && pcm, or cu_transquant_bypass)   */
-    void*            out[3];  /* decoded (post-SAO) planes Y, Cb, Cr; stride = plane width;
-                                 uint8_t samples (8-bit).  NULL = do not download              */
-    void*            recon[3];/* optional pre-SAO planes, same layout; NULL = skip             */
+    void*            out[3];  /* decoded (post-deblocking, post-SAO) planes Y, Cb, Cr; stride =
+                                 plane width; uint8_t samples (8-bit).  NULL = do not download */
+    void*            recon[3];/* optional in-loop-filter input (reconstruction before deblocking
+                                 and SAO), same layout; NULL = skip                             */
 } p265r_picture;
 
 /* Per-phase device time of the last run, from HIP events on the context's stream. */
@@ -121,7 +132,7 @@ typedef struct p265r_timings {
     double   total_ms;        /* first kernel start -> last kernel end                     */
     double   residual_ms;     /* dequant + inverse transform kernels                       */
     double   intra_ms;        /* intra prediction + reconstruction (all wavefront steps)   */
-    double   sao_ms;          /* SAO kernel                                                */
+    double   sao_ms;          /* in-loop filter kernel (deblocking + SAO)                  */
     int32_t  intra_launches;  /* kernel launches in the intra phase                        */
     int32_t  residual_launches;
     int32_t  sao_launches;

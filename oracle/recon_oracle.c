@@ -9,7 +9,8 @@
  * spec-form availability (6.4.1, global MinTbAddrZs), substitution (8.4.4.2.2),
  * filtering (8.4.4.2.3), planar/DC/angular (8.4.4.2.4-6), scaling (8.6.3), inverse
  * DCT/DST as plain O(N^3) matrix products (8.6.4.2), residual (8.6.2), construction
- * (8.6.7) and SAO (8.7.3).  Reference file:line for each piece: see the Python twin.
+ * (8.6.7), deblocking (8.7.2) and SAO (8.7.3).  Reference file:line for each piece: see
+ * the Python twin.
  *
  * Build: make -C oracle   ->  oracle/build/liboracle_p265.so
  */
@@ -309,6 +310,156 @@ static void sao(const geo_t* g, const p265r_params* prm, const p265r_picture* pi
     }
 }
 
+/* ---- deblocking (8.7.2; all-intra: bS = 2 on transform-block edges of the 8x8 grid) ---- */
+static const int BETA_T[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                               8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                               34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+static const int TC_T[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                             2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+static int qpc_of(int qpi) {
+    static const int T[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+    return qpi < 30 ? qpi : (qpi >= 43 ? qpi - 6 : T[qpi - 30]);
+}
+static inline int nib(int v) { return v >= 8 ? v - 16 : v; }
+
+typedef struct {
+    const geo_t* g;
+    const p265r_params* prm;
+    const uint8_t* nofilter;
+    int nfw, w4;
+    uint32_t* org;   /* per 4x4 luma unit: origin (x | y << 16) of the luma TB covering it */
+    uint8_t* qpy;    /* per 4x4 luma unit: QpY                                           */
+} dbk_t;
+
+/* bS == 2 && filterEdgeFlag for the edge between luma samples p0 (xp,yp) and q0 (xq,yq) */
+static int dbk_edge(const dbk_t* d, int xp, int yp, int xq, int yq) {
+    if (d->org[(yp >> 2) * d->w4 + (xp >> 2)] == d->org[(yq >> 2) * d->w4 + (xq >> 2)]) return 0;
+    const geo_t* g = d->g;
+    const int a = ctb_of(g, xq, yq), b = ctb_of(g, xp, yp);
+    const p265r_ctu* cq = &g->ctus[a];
+    if (!(cq->flags & P265R_CTU_DEBLOCK)) return 0;
+    if (a != b) {
+        if (!d->prm->loop_filter_across_tiles && g->ctus[b].tile_id != cq->tile_id) return 0;
+        if (g->ctus[b].slice_addr != cq->slice_addr && !(cq->flags & P265R_CTU_LF_ACROSS_SLICES)) return 0;
+    }
+    return 1;
+}
+static inline int dbk_nf(const dbk_t* d, int x, int y) { return d->nofilter && d->nofilter[(y >> 3) * d->nfw + (x >> 3)]; }
+static inline int dbk_qp(const dbk_t* d, int x, int y) { return d->qpy[(y >> 2) * d->w4 + (x >> 2)]; }
+
+/* s[i*step_i + k*step_k]: sample at distance i from the edge (i < 0: P side, p_i = s[-(i+1)]) on line k */
+static void dbk_luma_seg(uint8_t* s, int step_i, int step_k, int qpp, int qpq, int boff, int toff, int nop, int noq) {
+#define PS(i, k) s[-((i) + 1) * step_i + (k) * step_k]
+#define QS(i, k) s[(i) * step_i + (k) * step_k]
+    const int qpl = (qpq + qpp + 1) >> 1;
+    const int beta = BETA_T[clip3(0, 51, qpl + 2 * boff)];
+    const int tc = TC_T[clip3(0, 53, qpl + 2 + 2 * toff)];
+    const int dp0 = abs(PS(2, 0) - 2 * PS(1, 0) + PS(0, 0)), dp3 = abs(PS(2, 3) - 2 * PS(1, 3) + PS(0, 3));
+    const int dq0 = abs(QS(2, 0) - 2 * QS(1, 0) + QS(0, 0)), dq3 = abs(QS(2, 3) - 2 * QS(1, 3) + QS(0, 3));
+    if (dp0 + dq0 + dp3 + dq3 >= beta) return;
+    int strong = 1;
+    for (int j = 0; j < 2; ++j) {
+        const int k = j ? 3 : 0, dpq = 2 * (j ? dp3 + dq3 : dp0 + dq0);
+        if (!(dpq < (beta >> 2) && abs(PS(3, k) - PS(0, k)) + abs(QS(0, k) - QS(3, k)) < (beta >> 3) &&
+              abs(PS(0, k) - QS(0, k)) < ((5 * tc + 1) >> 1)))
+            strong = 0;
+    }
+    const int side = (beta + (beta >> 1)) >> 3;
+    const int dep = dp0 + dp3 < side, deq = dq0 + dq3 < side;
+    for (int k = 0; k < 4; ++k) {
+        const int p0 = PS(0, k), p1 = PS(1, k), p2 = PS(2, k), p3 = PS(3, k);
+        const int q0 = QS(0, k), q1 = QS(1, k), q2 = QS(2, k), q3 = QS(3, k);
+        if (strong) {
+            if (!nop) {
+                PS(0, k) = (uint8_t)clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+                PS(1, k) = (uint8_t)clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2);
+                PS(2, k) = (uint8_t)clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+            }
+            if (!noq) {
+                QS(0, k) = (uint8_t)clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+                QS(1, k) = (uint8_t)clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2);
+                QS(2, k) = (uint8_t)clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3);
+            }
+        } else {
+            int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+            if (abs(delta) >= tc * 10) continue;
+            delta = clip3(-tc, tc, delta);
+            if (!nop) {
+                PS(0, k) = (uint8_t)clip3(0, 255, p0 + delta);
+                if (dep) PS(1, k) = (uint8_t)clip3(0, 255, p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1));
+            }
+            if (!noq) {
+                QS(0, k) = (uint8_t)clip3(0, 255, q0 - delta);
+                if (deq) QS(1, k) = (uint8_t)clip3(0, 255, q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1));
+            }
+        }
+    }
+#undef PS
+#undef QS
+}
+
+static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture* pic, uint8_t* pl[3], const int stride[3]) {
+    int any = 0;
+    for (int i = 0; i < g->wc * g->hc; ++i) any |= g->ctus[i].flags & P265R_CTU_DEBLOCK;
+    if (!any) return;
+    dbk_t d;
+    d.g = g; d.prm = prm; d.nofilter = pic->nofilter; d.nfw = (g->w + 7) / 8; d.w4 = g->w >> 2;
+    const int h4 = g->h >> 2;
+    d.org = (uint32_t*)calloc((size_t)d.w4 * h4, sizeof(uint32_t));
+    d.qpy = (uint8_t*)calloc((size_t)d.w4 * h4, 1);
+    for (uint32_t t = 0; t < pic->n_tbs; ++t) {
+        const p265r_tb* tb = &pic->tbs[t];
+        if (tb->c_idx) continue;
+        const int n4 = 1 << (tb->log2_size - 2);
+        for (int j = 0; j < n4; ++j)
+            for (int i = 0; i < n4; ++i) {
+                const size_t u = (size_t)((tb->y >> 2) + j) * d.w4 + (tb->x >> 2) + i;
+                d.org[u] = (uint32_t)tb->x | (uint32_t)tb->y << 16;
+                d.qpy[u] = tb->qp;   /* 8-bit: QpBdOffsetY = 0 */
+            }
+    }
+    for (int dir = 0; dir < 2; ++dir) {          /* 0: vertical edges, 1: horizontal edges */
+        /* luma */
+        const int emax = dir ? g->h : g->w, smax = dir ? g->w : g->h;
+        for (int e = 8; e < emax; e += 8)
+            for (int s0 = 0; s0 < smax; s0 += 4) {
+                const int xq = dir ? s0 : e, yq = dir ? e : s0, xp = dir ? xq : xq - 1, yp = dir ? yq - 1 : yq;
+                if (!dbk_edge(&d, xp, yp, xq, yq)) continue;
+                const uint8_t off = g->ctus[ctb_of(g, xq, yq)].deblock_offsets;
+                uint8_t* s = pl[0] + (size_t)yq * stride[0] + xq;
+                dbk_luma_seg(s, dir ? stride[0] : 1, dir ? 1 : stride[0], dbk_qp(&d, xp, yp), dbk_qp(&d, xq, yq),
+                             nib(off & 15), nib(off >> 4), dbk_nf(&d, xp, yp), dbk_nf(&d, xq, yq));
+            }
+        /* chroma */
+        for (int c = 1; c < 3; ++c) {
+            const int cw = g->w >> 1, ch = g->h >> 1;
+            const int cemax = dir ? ch : cw, csmax = dir ? cw : ch;
+            const int cqp = c == 1 ? prm->pps_cb_qp_offset : prm->pps_cr_qp_offset;
+            for (int e = 8; e < cemax; e += 8)
+                for (int s0 = 0; s0 < csmax; s0 += 4) {
+                    const int xq = dir ? s0 : e, yq = dir ? e : s0;
+                    const int lxq = xq << 1, lyq = yq << 1, lxp = dir ? lxq : lxq - 1, lyp = dir ? lyq - 1 : lyq;
+                    if (!dbk_edge(&d, lxp, lyp, lxq, lyq)) continue;
+                    const int toff = nib(g->ctus[ctb_of(g, lxq, lyq)].deblock_offsets >> 4);
+                    const int qpc = qpc_of(((dbk_qp(&d, lxq, lyq) + dbk_qp(&d, lxp, lyp) + 1) >> 1) + cqp);
+                    const int tc = TC_T[clip3(0, 53, qpc + 2 + 2 * toff)];
+                    const int nop = dbk_nf(&d, lxp, lyp), noq = dbk_nf(&d, lxq, lyq);
+                    const int si = dir ? stride[c] : 1, sk = dir ? 1 : stride[c];
+                    for (int k = 0; k < 4; ++k) {
+                        uint8_t* q = pl[c] + (size_t)yq * stride[c] + xq + k * sk;
+                        const int p0 = q[-si], p1 = q[-2 * si], q0 = q[0], q1 = q[si];
+                        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
+                        if (!nop) q[-si] = (uint8_t)clip3(0, 255, p0 + delta);
+                        if (!noq) q[0] = (uint8_t)clip3(0, 255, q0 - delta);
+                    }
+                }
+        }
+    }
+    free(d.org);
+    free(d.qpy);
+}
+
 /* Decode n pictures: writes pics[i].recon[] (if set) and pics[i].out[] (if set).
  * Returns 0 or a negative P265R_* code.  n_threads <= 0: OpenMP default. */
 int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int n_threads) {
@@ -343,10 +494,19 @@ int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int
                 recon_tb(&g, prm, rec, stride, &pics[i].tbs[k], pics[i].coef);
         }
         if (out[0] && out[1] && out[2]) {
-            if (prm->sample_adaptive_offset) sao(&g, prm, &pics[i], rec, out, stride);
+            /* in-loop filters: deblocking into a scratch copy (rec stays the filter input), then SAO */
+            uint8_t* dbk[3];
+            for (int c = 0; c < 3; ++c) {
+                const size_t sz = (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height);
+                dbk[c] = (uint8_t*)malloc(sz);
+                memcpy(dbk[c], rec[c], sz);
+            }
+            deblock(&g, prm, &pics[i], dbk, stride);
+            if (prm->sample_adaptive_offset) sao(&g, prm, &pics[i], dbk, out, stride);
             else
                 for (int c = 0; c < 3; ++c)
-                    memcpy(out[c], rec[c], (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height));
+                    memcpy(out[c], dbk[c], (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height));
+            for (int c = 0; c < 3; ++c) free(dbk[c]);
         }
         for (int c = 0; c < 3; ++c) if (!pics[i].recon[c]) free(rec[c]);
         free(order);

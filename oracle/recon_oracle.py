@@ -14,6 +14,8 @@ follows is cited in its docstring):
   * 8.4.4.2.4-6 planar / DC / angular       <- decoder/intra.py:82-184
   * 8.6.7 picture construction (clip)       <- decoder/reconstruction.py:4-27
   * 6.4.1 z-scan availability               <- decoder/image.py:38-73, pps.py:246-262
+  * 8.7.2 deblocking (absent in the reference: pps.py:122-131 / slice.py:170-179 parse
+    its controls, no filter exists)
   * 8.7.3 SAO (absent in the reference; sao.py:15-136 is syntax only)
 
 Parity status: the front-end records that feed this oracle are pinned by the
@@ -22,7 +24,7 @@ planar, DC, horizontal-family angular, modes 18/26/34, neighbour filtering and
 scaling functions are pinned against outputs of the reference's own functions
 (tests/golden/gen_component_fixture.py).  The inverse transform, the vertical
 angular modes the reference gets wrong, substitution when the bottom-left sample
-is present, and SAO filtering have no reference output to pin against: for those
+is present, deblocking and SAO filtering have no reference output to pin against: for those
 parity is UNPINNED by the reference and rests on spec restatement + known-answer
 tests (tests/test_oracle_kat.py).
 
@@ -73,7 +75,22 @@ INV_ANGLE = [-4096, -1638, -910, -630, -482, -390, -315, -256, -315, -390, -482,
 LEVEL_SCALE = [40, 45, 51, 57, 64, 72]   # scaling.py:28
 
 TB_CBF, TB_TSKIP, TB_BYPASS, TB_PCM = 1, 2, 4, 8
-CTU_LF_ACROSS_SLICES = 1
+CTU_LF_ACROSS_SLICES, CTU_DEBLOCK = 1, 2
+
+# Table 8-12: beta' (Q = 0..51) and tC' (Q = 0..53)
+BETA_TABLE = [0] * 16 + list(range(6, 19)) + list(range(20, 65, 2))
+TC_TABLE = ([0] * 18 + [1] * 9 + [2] * 4 + [3] * 4 + [4] * 3 + [5] * 2 + [6] * 2
+            + [7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24])
+assert len(BETA_TABLE) == 52 and len(TC_TABLE) == 54
+
+
+def qpc_from_qpi(qpi):
+    """Table 8-10 (ChromaArrayType == 1); the reference's copy is cu.py:575-591."""
+    if qpi < 30:
+        return qpi
+    if qpi >= 43:
+        return qpi - 6
+    return [29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37][qpi - 30]
 
 
 def transform_matrix(log2, tr_type):
@@ -345,14 +362,14 @@ def _recon_tb(geo, planes, t, coef, bd, strong):
 
 
 # ---------------------------------------------------------------------------
-# SAO 8.7.3 (CTB granularity; pre-deblocking input)
+# SAO 8.7.3 (CTB granularity; input = the deblocked picture)
 # ---------------------------------------------------------------------------
 
 _EO_POS = [((-1, 0), (1, 0)), ((0, -1), (0, 1)), ((-1, -1), (1, 1)), ((1, -1), (-1, 1))]  # (dx, dy)
 
 
 def sao_picture(params, pic, recon):
-    """Apply SAO to pre-SAO planes ``recon`` -> new planes (8.7.3.1-8.7.3.2)."""
+    """Apply SAO to the deblocked planes ``recon`` -> new planes (8.7.3.1-8.7.3.2)."""
     geo = Geometry(params, pic["ctus"])
     out = [r.copy() for r in recon]
     if not int(params["sample_adaptive_offset"]):
@@ -422,7 +439,201 @@ def sao_picture(params, pic, recon):
     return out
 
 
+# ---------------------------------------------------------------------------
+# Deblocking 8.7.2 (all-intra: bS = 2 on every transform-block edge of the 8x8 grid)
+# ---------------------------------------------------------------------------
+
+def _clip3(lo, hi, v):
+    return lo if v < lo else (hi if v > hi else v)
+
+
+def deblock_luma_segment(p, q, qp_p, qp_q, beta_offset_div2, tc_offset_div2, no_p, no_q, bit_depth=8, bs=2):
+    """One 4-line luma edge segment: decisions 8.7.2.5.3 / 8.7.2.5.6, filtering 8.7.2.5.7.
+
+    p[i][k], q[i][k]: sample i away from the edge (i = 0..3) on line k (k = 0..3).
+    Returns new (p, q) as lists of lists (only p0..p2 / q0..q2 can change).
+    """
+    p = [list(map(int, r)) for r in p]
+    q = [list(map(int, r)) for r in q]
+    qpl = (qp_q + qp_p + 1) >> 1
+    beta = BETA_TABLE[_clip3(0, 51, qpl + (beta_offset_div2 << 1))] * (1 << (bit_depth - 8))
+    tc = TC_TABLE[_clip3(0, 53, qpl + 2 * (bs - 1) + (tc_offset_div2 << 1))] * (1 << (bit_depth - 8))
+    dp0 = abs(p[2][0] - 2 * p[1][0] + p[0][0])
+    dp3 = abs(p[2][3] - 2 * p[1][3] + p[0][3])
+    dq0 = abs(q[2][0] - 2 * q[1][0] + q[0][0])
+    dq3 = abs(q[2][3] - 2 * q[1][3] + q[0][3])
+    dpq0, dpq3 = dp0 + dq0, dp3 + dq3
+    dp, dq = dp0 + dp3, dq0 + dq3
+    d = dpq0 + dpq3
+    if d >= beta:
+        return p, q
+
+    def dsam(k, dpq):
+        return (dpq < (beta >> 2) and abs(p[3][k] - p[0][k]) + abs(q[0][k] - q[3][k]) < (beta >> 3)
+                and abs(p[0][k] - q[0][k]) < ((5 * tc + 1) >> 1))
+
+    strong = dsam(0, 2 * dpq0) and dsam(3, 2 * dpq3)
+    dep = dp < ((beta + (beta >> 1)) >> 3)
+    deq = dq < ((beta + (beta >> 1)) >> 3)
+    maxv = (1 << bit_depth) - 1
+    for k in range(4):
+        p0, p1, p2, p3 = p[0][k], p[1][k], p[2][k], p[3][k]
+        q0, q1, q2, q3 = q[0][k], q[1][k], q[2][k], q[3][k]
+        if strong:
+            np_ = [_clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3),
+                   _clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2),
+                   _clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3)]
+            nq = [_clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3),
+                  _clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2),
+                  _clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3)]
+            ndp = ndq = 3
+        else:
+            delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4
+            if abs(delta) >= tc * 10:
+                continue
+            delta = _clip3(-tc, tc, delta)
+            np_ = [_clip3(0, maxv, p0 + delta), p1, p2]
+            nq = [_clip3(0, maxv, q0 - delta), q1, q2]
+            if dep:
+                np_[1] = _clip3(0, maxv, p1 + _clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1))
+            if deq:
+                nq[1] = _clip3(0, maxv, q1 + _clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1))
+            ndp, ndq = (2 if dep else 1), (2 if deq else 1)
+        if no_p:
+            ndp = 0
+        if no_q:
+            ndq = 0
+        for i in range(ndp):
+            p[i][k] = np_[i]
+        for i in range(ndq):
+            q[i][k] = nq[i]
+    return p, q
+
+
+def deblock_chroma_line(p0, p1, q0, q1, tc, no_p, no_q, bit_depth=8):
+    """8.7.2.5.5 filtering of one chroma line across an edge (bS = 2)."""
+    maxv = (1 << bit_depth) - 1
+    delta = _clip3(-tc, tc, ((((q0 - p0) << 2) + p1 - q1 + 4) >> 3))
+    return (p0 if no_p else _clip3(0, maxv, p0 + delta)), (q0 if no_q else _clip3(0, maxv, q0 - delta))
+
+
+def chroma_tc(qp_p, qp_q, c_qp_pic_offset, tc_offset_div2, bit_depth=8):
+    """tC of a chroma edge (8.7.2.5.5): QpC from Table 8-10 on ((QpQ + QpP + 1) >> 1) + cQpPicOffset."""
+    qpc = qpc_from_qpi(((qp_q + qp_p + 1) >> 1) + c_qp_pic_offset)
+    return TC_TABLE[_clip3(0, 53, qpc + 2 + (tc_offset_div2 << 1))] * (1 << (bit_depth - 8))
+
+
+def _unpack_offsets(v):
+    b, t = int(v) & 15, (int(v) >> 4) & 15
+    return (b - 16 if b >= 8 else b), (t - 16 if t >= 8 else t)
+
+
+def deblock_picture(params, pic, recon):
+    """8.7.2 deblocking of the reconstructed planes -> new planes [Y, Cb, Cr].
+
+    Edges: luma transform-block boundaries (the spec's transform and, for intra NxN,
+    prediction edges; the latter sit at 4-sample offsets and never reach the 8x8 grid)
+    on the 8x8 luma grid, found here from a per-4x4 map of TB indices.  bS = 2 for every
+    edge (all-intra).  All vertical edges of the picture are filtered first (input: the
+    reconstruction), then all horizontal edges (input: the vertically filtered picture).
+    filterEdgeFlag (8.7.2.3): no edge on the picture boundary; at a tile boundary only
+    with loop_filter_across_tiles; at a slice boundary only with the flag of the slice
+    containing q0; no edge owned by a CTU whose slice has deblocking disabled.  The
+    slice's offsets are those of the CTU containing q0.
+    """
+    ctus = pic["ctus"]
+    out = [np.array(r, np.int64, copy=True) for r in recon]
+    if not (np.asarray(ctus["flags"]) & CTU_DEBLOCK).any():
+        return out
+    geo = Geometry(params, ctus)
+    w, h = geo.w, geo.h
+    bd = [int(params["bit_depth_luma"]), int(params["bit_depth_chroma"]), int(params["bit_depth_chroma"])]
+    lf_tiles = bool(params["loop_filter_across_tiles"])
+    cqp = [0, int(params.get("pps_cb_qp_offset", 0)), int(params.get("pps_cr_qp_offset", 0))]
+    tbid = np.full((h >> 2, w >> 2), -1, np.int64)
+    qp4 = np.zeros((h >> 2, w >> 2), np.int64)
+    for i, t in enumerate(pic["tbs"]):
+        if int(t["c_idx"]) != 0:
+            continue
+        x4, y4, n4 = int(t["x"]) >> 2, int(t["y"]) >> 2, 1 << (int(t["log2_size"]) - 2)
+        tbid[y4:y4 + n4, x4:x4 + n4] = i
+        qp4[y4:y4 + n4, x4:x4 + n4] = int(t["qp"]) - 6 * (bd[0] - 8)     # QpY = Qp'Y - QpBdOffsetY
+    nofilter = pic.get("nofilter")
+    nfw = (w + 7) >> 3
+
+    def nf(x, y):
+        return nofilter is not None and bool(nofilter[(y >> 3) * nfw + (x >> 3)])
+
+    def edge_ok(xp, yp, xq, yq):
+        """bS = 2 and filterEdgeFlag for the luma positions of p0 and q0."""
+        if tbid[yp >> 2, xp >> 2] == tbid[yq >> 2, xq >> 2]:
+            return False
+        a, b = geo.ctb_of(xq, yq), geo.ctb_of(xp, yp)
+        cq = ctus[a]
+        if not (int(cq["flags"]) & CTU_DEBLOCK):
+            return False
+        if a != b:
+            if not lf_tiles and geo.tile[a] != geo.tile[b]:
+                return False
+            if geo.slice_addr[a] != geo.slice_addr[b] and not (int(cq["flags"]) & CTU_LF_ACROSS_SLICES):
+                return False
+        return True
+
+    for vertical in (True, False):
+        # ---- luma: edges every 8 samples, 4-line segments ----------------------------
+        Y = out[0]
+        e_max, s_max = (w, h) if vertical else (h, w)
+        for e in range(8, e_max, 8):
+            for s0 in range(0, s_max, 4):
+                xq, yq = (e, s0) if vertical else (s0, e)
+                xp, yp = (e - 1, s0) if vertical else (s0, e - 1)
+                if not edge_ok(xp, yp, xq, yq):
+                    continue
+                beta_off, tc_off = _unpack_offsets(ctus[geo.ctb_of(xq, yq)]["deblock_offsets"])
+                if vertical:
+                    P = [[Y[s0 + k, e - 1 - i] for k in range(4)] for i in range(4)]
+                    Q = [[Y[s0 + k, e + i] for k in range(4)] for i in range(4)]
+                else:
+                    P = [[Y[e - 1 - i, s0 + k] for k in range(4)] for i in range(4)]
+                    Q = [[Y[e + i, s0 + k] for k in range(4)] for i in range(4)]
+                P, Q = deblock_luma_segment(P, Q, qp4[yp >> 2, xp >> 2], qp4[yq >> 2, xq >> 2], beta_off, tc_off,
+                                            nf(xp, yp), nf(xq, yq), bd[0])
+                for i in range(3):
+                    for k in range(4):
+                        if vertical:
+                            Y[s0 + k, e - 1 - i], Y[s0 + k, e + i] = P[i][k], Q[i][k]
+                        else:
+                            Y[e - 1 - i, s0 + k], Y[e + i, s0 + k] = P[i][k], Q[i][k]
+        # ---- chroma (4:2:0): edges every 8 chroma samples, bS of the luma edge at 2x --------
+        for c in (1, 2):
+            C = out[c]
+            ch, cw = C.shape
+            e_max, s_max = (cw, ch) if vertical else (ch, cw)
+            for e in range(8, e_max, 8):
+                for s0 in range(0, s_max, 4):
+                    xq, yq = ((e, s0) if vertical else (s0, e))
+                    xp, yp = ((e - 1, s0) if vertical else (s0, e - 1))
+                    lq = (xq << 1, yq << 1)
+                    lp = ((xq << 1) - 1, yq << 1) if vertical else (xq << 1, (yq << 1) - 1)
+                    if not edge_ok(lp[0], lp[1], lq[0], lq[1]):
+                        continue
+                    _, tc_off = _unpack_offsets(ctus[geo.ctb_of(*lq)]["deblock_offsets"])
+                    tc = chroma_tc(qp4[lp[1] >> 2, lp[0] >> 2], qp4[lq[1] >> 2, lq[0] >> 2], cqp[c], tc_off, bd[c])
+                    no_p, no_q = nf(*lp), nf(*lq)
+                    for k in range(4):
+                        if vertical:
+                            r = s0 + k
+                            C[r, e - 1], C[r, e] = deblock_chroma_line(C[r, e - 1], C[r, e - 2], C[r, e], C[r, e + 1],
+                                                                       tc, no_p, no_q, bd[c])
+                        else:
+                            x = s0 + k
+                            C[e - 1, x], C[e, x] = deblock_chroma_line(C[e - 1, x], C[e - 2, x], C[e, x], C[e + 1, x],
+                                                                       tc, no_p, no_q, bd[c])
+    return out
+
+
 def decode_picture(params, pic):
-    """Pre-SAO recon followed by SAO. Returns (recon, out), each [Y, Cb, Cr]."""
+    """Reconstruction, then the in-loop filters (deblocking, SAO).  Returns (recon, out),
+    each [Y, Cb, Cr]: recon is the deblocking input, out the decoded picture."""
     rec = reconstruct_picture(params, pic)
-    return rec, sao_picture(params, pic, rec)
+    return rec, sao_picture(params, pic, deblock_picture(params, pic, rec))

@@ -41,7 +41,8 @@ class Params(ctypes.Structure):
                 ("min_tb_log2_size", ctypes.c_uint8), ("max_tb_log2_size", ctypes.c_uint8),
                 ("strong_intra_smoothing", ctypes.c_uint8), ("constrained_intra_pred", ctypes.c_uint8),
                 ("sample_adaptive_offset", ctypes.c_uint8), ("loop_filter_across_tiles", ctypes.c_uint8),
-                ("scaling_list_enabled", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 13)]
+                ("scaling_list_enabled", ctypes.c_uint8), ("pps_cb_qp_offset", ctypes.c_int8),
+                ("pps_cr_qp_offset", ctypes.c_int8), ("reserved", ctypes.c_uint8 * 11)]
 
 
 class PictureC(ctypes.Structure):

@@ -38,6 +38,7 @@ struct DevPic {                 // per picture, device-resident table
     const uint8_t* nofilter;    // per 8x8 luma block or nullptr
     IntraJob* jobs;             // same index space as tbs (jobs of a CTU start at tb_begin)
     uint32_t* jcount;           // per CTU: number of jobs
+    uint8_t* dbk_map;           // per 8x8 luma block (loopfilter.h), nullptr without deblocking
 };
 
 struct Geo {                    // batch-uniform geometry
@@ -48,7 +49,8 @@ struct Geo {                    // batch-uniform geometry
     int bd[3];
     int strong;
     int lf_tiles;
-    int nf_w;                   // nofilter map width (ceil(w/8))
+    int nf_w;                   // nofilter / deblocking map width (ceil(w/8))
+    int cqp[2];                 // pps_cb_qp_offset, pps_cr_qp_offset (chroma deblocking)
 };
 
 __constant__ int8_t  c_angle[35];

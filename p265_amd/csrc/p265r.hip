@@ -21,6 +21,7 @@
 #include "intra.h"
 #include "intra_prep.h"
 #include "intra_rows.h"
+#include "loopfilter.h"
 #include "residual.h"
 #include "sao.h"
 #include "tables.h"
@@ -81,6 +82,7 @@ struct p265r_ctx {
     int row_waves = 16;        // waves per workgroup of the row pipeline (4, 8 or 16)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
+    bool lf_kernel = true;     // SAO-only batches: windowed loopfilter_kernel (1) or sao_kernel (0); P265R_SAO_KERNEL
 };
 
 struct p265r_batch {
@@ -95,6 +97,7 @@ struct p265r_batch {
     int n_jobs[RC_NUM] = {};
     std::vector<DevPic> h_pics;
     bool sao = false;
+    bool dbk = false;          // some CTU of the batch has deblocking on
 };
 
 namespace {
@@ -107,6 +110,10 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     for (int rs = 0; rs < ctx->n_ctus; ++rs) {
         const p265r_ctu& c = pic.ctus[rs];
         if ((uint64_t)c.tb_begin + c.tb_count > pic.n_tbs) return P265R_ERANGE;
+        for (int k = 0; k < 2; ++k) {
+            const int v = ((c.deblock_offsets >> (4 * k)) & 15) ^ 8;   // biased: -6..6 -> 2..14
+            if (v < 2 || v > 14) return P265R_EINVAL;
+        }
         for (int k = 0; k < 3; ++k) {
             if (c.sao_type[k] > 2) return P265R_EINVAL;
             if (c.sao_type[k] == 2 && c.sao_class[k] > 3) return P265R_EINVAL;
@@ -239,9 +246,12 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.strong = p.strong_intra_smoothing;
     g.lf_tiles = p.loop_filter_across_tiles;
     g.nf_w = (g.w + 7) / 8;
+    g.cqp[0] = p.pps_cb_qp_offset;
+    g.cqp[1] = p.pps_cr_qp_offset;
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
+    if (const char* v = std::getenv("P265R_SAO_KERNEL")) ctx->lf_kernel = std::strcmp(v, "direct") != 0;
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 8 || w == 16) ctx->row_waves = w;
@@ -310,6 +320,11 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         }
     // ---- device layout -----------------------------------------------------------
     const bool sao = ctx->params.sample_adaptive_offset != 0;
+    bool dbk = false;
+    for (int i = 0; i < n_pics && !dbk; ++i)
+        for (int rs = 0; rs < nc; ++rs)
+            if (pics[i].ctus[rs].flags & P265R_CTU_DEBLOCK) { dbk = true; break; }
+    const bool lf = sao || dbk;                  // separate output planes
     const size_t plane_bytes[3] = {(size_t)g.stride[0] * g.h, (size_t)g.stride[1] * g.ch, (size_t)g.stride[2] * g.ch};
     const size_t pic_plane_bytes = align_up(plane_bytes[0], 256) + 2 * align_up(plane_bytes[1], 256);
     size_t off = 0;
@@ -330,8 +345,9 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     size_t n_nf = 0;
     for (int i = 0; i < n_pics; ++i) n_nf += pics[i].nofilter ? 1 : 0;
     off = align_up(off + nf_bytes * n_nf, 256);
+    const size_t o_map = off; if (dbk) off = align_up(off + nf_bytes * n_pics, 256);
     const size_t o_rec = off; off += pic_plane_bytes * n_pics;
-    const size_t o_out = off; if (sao) off += pic_plane_bytes * n_pics;
+    const size_t o_out = off; if (lf) off += pic_plane_bytes * n_pics;
     const size_t total = align_up(off, 256);
 
     // ---- host staging ------------------------------------------------------------
@@ -345,6 +361,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->bytes = total;
     b->n_pics = n_pics;
     b->sao = sao;
+    b->dbk = dbk;
     unsigned char* dbase = static_cast<unsigned char*>(b->mem);
     b->d_pics = reinterpret_cast<DevPic*>(dbase + o_pics);
     b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
@@ -387,7 +404,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         dp.rec[0] = rec;
         dp.rec[1] = rec + align_up(plane_bytes[0], 256);
         dp.rec[2] = dp.rec[1] + align_up(plane_bytes[1], 256);
-        if (sao) {
+        dp.dbk_map = dbk ? dbase + o_map + nf_bytes * i : nullptr;
+        if (lf) {
             unsigned char* o = dbase + o_out + pic_plane_bytes * i;
             dp.out[0] = o;
             dp.out[1] = o + align_up(plane_bytes[0], 256);
@@ -450,6 +468,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
         ++tm.residual_launches;
     }
+    if (b->dbk) {
+        // deblocking edge / QpY map: depends on the records only
+        dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
+        ++tm.residual_launches;
+    }
     HIP_TRY(hipGetLastError());
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] residual phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] residual phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
@@ -473,8 +496,21 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     HIP_TRY(hipGetLastError());
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
-    // ---- SAO -----------------------------------------------------------------------
-    if (b->sao) {
+    // ---- in-loop filters: deblocking + SAO ----------------------------------------------
+    if (b->dbk || (b->sao && ctx->lf_kernel)) {
+        const dim3 grid(ctx->n_ctus, b->n_pics);
+        const int so = b->sao ? 1 : 0;
+        switch (g.ctb_log2 * 2 + (b->dbk ? 1 : 0)) {
+            case 12: loopfilter_kernel<6, false><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so); break;
+            case 13: loopfilter_kernel<6, true><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so); break;
+            case 10: loopfilter_kernel<5, false><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so); break;
+            case 11: loopfilter_kernel<5, true><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so); break;
+            case 8: loopfilter_kernel<4, false><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so); break;
+            default: loopfilter_kernel<4, true><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so); break;
+        }
+        ++tm.sao_launches;
+        HIP_TRY(hipGetLastError());
+    } else if (b->sao) {
         const int cs = 1 << g.ctb_log2;
         if (g.ctb_log2 >= 5) {
             const int threads = (cs / 16) * cs + 2 * (cs / 32) * (cs / 2);

@@ -115,7 +115,8 @@ class PictureBuilder:
                 lg = log2 if c == 0 else log2 - 1
                 sub = 0 if c == 0 else 1
                 off = self._store(pcm_samples[c])
-                self._tb(addr, x >> sub, y >> sub, lg, c, 0, R.TB_PCM, 0, off)
+                # qp of a PCM TB is not used for scaling; the luma one carries QpY for deblocking
+                self._tb(addr, x >> sub, y >> sub, lg, c, 0, R.TB_PCM, (qp_y, qp_cb, qp_cr)[c], off)
             return
         half = (1 << log2) >> 1
         for t in tus:
@@ -145,11 +146,15 @@ class PictureBuilder:
 
     # -- the per-CTU hook (Ctu.parse after Sao.parse) -------------------------
     def add_ctu(self, addr, slice_addr=0, tile_id=0, lf_across_slices=True,
-                sao_type=(0, 0, 0), sao_abs=None, sao_sign=None, sao_band=(0, 0, 0), sao_eo=(0, 0, 0)):
+                sao_type=(0, 0, 0), sao_abs=None, sao_sign=None, sao_band=(0, 0, 0), sao_eo=(0, 0, 0),
+                deblocking=False, beta_offset_div2=0, tc_offset_div2=0):
+        """``deblocking``: !slice_deblocking_filter_disabled_flag of the CTU's slice, with its
+        slice_beta_offset_div2 / slice_tc_offset_div2 (slice.py:170-175, pps.py:122-131)."""
         c = self.ctus[addr]
         c["slice_addr"] = slice_addr
         c["tile_id"] = tile_id
-        c["flags"] = R.CTU_LF_ACROSS_SLICES if lf_across_slices else 0
+        c["flags"] = (R.CTU_LF_ACROSS_SLICES if lf_across_slices else 0) | (R.CTU_DEBLOCK if deblocking else 0)
+        c["deblock_offsets"] = R.deblock_offsets(int(beta_offset_div2), int(tc_offset_div2)) if deblocking else 0
         for ci in range(3):
             t = int(sao_type[ci])
             c["sao_type"][ci] = t
@@ -220,7 +225,18 @@ class ReconHook:
     def on_ctu_parsed(self, ctu, slice_hdr):
         s = ctu.sao
         on = bool(slice_hdr.slice_sao_luma_flag or slice_hdr.slice_sao_chroma_flag)
+        # slice_deblocking_filter_disabled_flag is never assigned by the reference (slice.py:170-178
+        # reads it); absent an override it is inferred from the PPS (pps.py:122-131)
+        pps = getattr(slice_hdr, "pps", None)
+        dbk_off = bool(getattr(slice_hdr, "slice_deblocking_filter_disabled_flag",
+                               getattr(pps, "pps_deblocking_filter_disabled_flag", 0)))
         self.builder.add_ctu(ctu.addr_rs, slice_addr=getattr(ctu, "slice_addr", 0),
+                             lf_across_slices=bool(getattr(slice_hdr, "slice_loop_filter_across_slices_enabled_flag", 1)),
+                             deblocking=not dbk_off,
+                             beta_offset_div2=int(getattr(slice_hdr, "slice_beta_offset_div2",
+                                                          getattr(pps, "pps_beta_offset_div2", 0))),
+                             tc_offset_div2=int(getattr(slice_hdr, "slice_tc_offset_div2",
+                                                        getattr(pps, "pps_tc_offset_div2", 0))),
                              sao_type=s.sao_type_idx if on else (0, 0, 0),
                              sao_abs=s.sao_offset_abs if on else None,
                              sao_sign=s.sao_offset_sign if on else None,
@@ -241,14 +257,21 @@ def params_from_frontend(d):
         ctb_log2_size=d["ctb_log2_size"], min_tb_log2_size=d["min_tb_log2_size"],
         max_tb_log2_size=d["max_tb_log2_size"], strong_intra_smoothing=d["strong_intra_smoothing"],
         constrained_intra_pred=d["constrained_intra_pred"], sample_adaptive_offset=d["sample_adaptive_offset"],
-        loop_filter_across_tiles=d["loop_filter_across_tiles"], scaling_list_enabled=d["scaling_list_enabled"])
+        loop_filter_across_tiles=d["loop_filter_across_tiles"], scaling_list_enabled=d["scaling_list_enabled"],
+        pps_cb_qp_offset=d.get("pps_cb_qp_offset", 0), pps_cr_qp_offset=d.get("pps_cr_qp_offset", 0))
 
 
-def pictures_from_frontend_npz(path):
-    """Rebuild (params, [Picture]) from tests/golden/sanity_frontend.npz."""
+def pictures_from_frontend_npz(path, deblocking=None):
+    """Rebuild (params, [Picture]) from tests/golden/sanity_frontend.npz.
+
+    ``deblocking`` None follows the stream: sanity.bin has deblocking_filter_control_present_flag
+    = 0 (test/golden/pps.log:23), i.e. deblocking on with zero offsets in every slice.
+    """
     z = np.load(path, allow_pickle=False)
     pd = json.loads(bytes(z["params"]).decode())
     params = params_from_frontend(pd)
+    if deblocking is None:
+        deblocking = not pd.get("deblocking_filter_control_present", 0)
     cus, tus, coefs, ctus = z["cus"], z["tus"], z["coefs"], z["ctus"]
     # dense coefficient blocks per (tu, c): [y][x]
     blocks = {}
@@ -280,6 +303,6 @@ def pictures_from_frontend_npz(path):
         for r in ctus[ctus["frame"] == f]:
             b.add_ctu(int(r["ctu"]), slice_addr=int(r["slice_addr"]), lf_across_slices=bool(r["lf_across_slices"]),
                       sao_type=r["sao_type"], sao_abs=r["sao_abs"], sao_sign=r["sao_sign"],
-                      sao_band=r["sao_band"], sao_eo=r["sao_eo"])
+                      sao_band=r["sao_band"], sao_eo=r["sao_eo"], deblocking=deblocking)
         pics.append(b.finish(meta={"source": "sanity.bin", "frame": f}))
     return params, pics

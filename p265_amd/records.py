@@ -20,7 +20,7 @@ import numpy as np
 ABI_VERSION = 1
 
 TB_CBF, TB_TSKIP, TB_BYPASS, TB_PCM = 0x01, 0x02, 0x04, 0x08
-CTU_LF_ACROSS_SLICES = 0x01
+CTU_LF_ACROSS_SLICES, CTU_DEBLOCK = 0x01, 0x02
 
 PARAMS_DTYPE = np.dtype([
     ("version", "<u4"), ("pic_width", "<u2"), ("pic_height", "<u2"),
@@ -28,12 +28,13 @@ PARAMS_DTYPE = np.dtype([
     ("ctb_log2_size", "u1"), ("min_tb_log2_size", "u1"), ("max_tb_log2_size", "u1"),
     ("strong_intra_smoothing", "u1"), ("constrained_intra_pred", "u1"),
     ("sample_adaptive_offset", "u1"), ("loop_filter_across_tiles", "u1"),
-    ("scaling_list_enabled", "u1"), ("reserved", "u1", 13)])
+    ("scaling_list_enabled", "u1"), ("pps_cb_qp_offset", "i1"), ("pps_cr_qp_offset", "i1"),
+    ("reserved", "u1", 11)])
 assert PARAMS_DTYPE.itemsize == 32
 
 CTU_DTYPE = np.dtype([
     ("tb_begin", "<u4"), ("tb_count", "<u2"), ("tile_id", "<u2"), ("slice_addr", "<u4"),
-    ("flags", "u1"), ("sao_type", "u1", 3), ("sao_class", "u1", 3), ("reserved", "u1"),
+    ("flags", "u1"), ("sao_type", "u1", 3), ("sao_class", "u1", 3), ("deblock_offsets", "u1"),
     ("sao_offset", "i1", (3, 4))])
 assert CTU_DTYPE.itemsize == 32
 
@@ -50,7 +51,7 @@ def make_params(**kw) -> np.ndarray:
     d = dict(pic_width=352, pic_height=288, chroma_format_idc=1, bit_depth_luma=8,
              bit_depth_chroma=8, ctb_log2_size=6, min_tb_log2_size=2, max_tb_log2_size=5,
              strong_intra_smoothing=1, constrained_intra_pred=0, sample_adaptive_offset=1,
-             loop_filter_across_tiles=1, scaling_list_enabled=0)
+             loop_filter_across_tiles=1, scaling_list_enabled=0, pps_cb_qp_offset=0, pps_cr_qp_offset=0)
     for k, v in kw.items():
         if k not in d:
             raise KeyError("unknown params field %r" % k)
@@ -60,6 +61,20 @@ def make_params(**kw) -> np.ndarray:
     for k, v in d.items():
         p[k] = v
     return p
+
+
+def deblock_offsets(beta_offset_div2, tc_offset_div2) -> int:
+    """P265R_DEBLOCK_OFFSETS: two 4-bit two's-complement fields (each -6..6)."""
+    for v in (beta_offset_div2, tc_offset_div2):
+        if not -6 <= v <= 6:
+            raise ValueError("deblocking offset_div2 out of range: %d" % v)
+    return (beta_offset_div2 & 15) | ((tc_offset_div2 & 15) << 4)
+
+
+def unpack_deblock_offsets(v):
+    """(slice_beta_offset_div2, slice_tc_offset_div2) of a CTU record's deblock_offsets byte."""
+    b, t = int(v) & 15, (int(v) >> 4) & 15
+    return (b - 16 if b >= 8 else b), (t - 16 if t >= 8 else t)
 
 
 def params_dict(p) -> dict:
@@ -134,5 +149,8 @@ def validate(params, pic: Picture):
         raise RecordError("coefficient range outside coef array")
     if (pic.ctus["sao_type"] > 2).any():
         raise RecordError("bad SaoTypeIdx")
+    nib = np.stack([pic.ctus["deblock_offsets"] & 15, pic.ctus["deblock_offsets"] >> 4])
+    if ((nib == 7) | (nib == 8) | (nib == 9)).any():
+        raise RecordError("deblocking offset_div2 outside -6..6")
     if pic.nofilter is not None and len(pic.nofilter) != ((w + 7) // 8) * ((h + 7) // 8):
         raise RecordError("nofilter map has the wrong size")

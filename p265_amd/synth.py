@@ -55,14 +55,19 @@ def uniform_tiles(wc, hc, cols, rows):
 
 
 def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, tskip_rate=0.008,
-                 bypass_rate=0.0, lf_across_slices=True):
-    """One synthetic picture (records.Picture) for ``params``."""
+                 bypass_rate=0.0, lf_across_slices=True, deblocking=False, pcm_rate=0.0):
+    """One synthetic picture (records.Picture) for ``params``.
+
+    ``deblocking``: False (SURVEY §8(d) perf config), True (on, zero offsets) or "random"
+    (per slice: on with probability 0.8, slice_beta/tc_offset_div2 uniform in -6..6).
+    ``pcm_rate``: fraction of 8x8..32x32 CUs coded as PCM with pcm_loop_filter_disabled.
+    """
     rng = np.random.default_rng(seed)
     p = params
     w, h = int(p["pic_width"]), int(p["pic_height"])
     ctb_log2 = int(p["ctb_log2_size"])
     wc, hc = R.ctb_grid(p)
-    b = frontend.PictureBuilder(p)
+    b = frontend.PictureBuilder(p, pcm_loop_filter_disabled=pcm_rate > 0)
     tile = uniform_tiles(wc, hc, *tiles)
     order = np.lexsort((np.arange(wc * hc), tile))          # tile-scan order
     # slices: contiguous runs in tile-scan order
@@ -78,6 +83,10 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
         slice_addr_ts[ts] = first[s]
     slice_lf = {s: (lf_across_slices if isinstance(lf_across_slices, bool) else bool(rng.integers(0, 2)))
                 for s in first}
+    if deblocking == "random":
+        slice_dbk = {s: (bool(rng.random() < 0.8), int(rng.integers(-6, 7)), int(rng.integers(-6, 7))) for s in first}
+    else:
+        slice_dbk = {s: (bool(deblocking), 0, 0) for s in first}
     max_tb = int(p["max_tb_log2_size"])
     flat_bias = 0.0 if perf else 0.3
 
@@ -136,6 +145,11 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
                 cu_tree(x + hlf * (i % 2), y + hlf * (i // 2), log2 - 1)
             return
         qy, qcb, qcr = qps()
+        if pcm_rate > 0 and log2 <= 5 and rng.random() < pcm_rate:
+            n = 1 << log2
+            smp = [rng.integers(0, 256, (n >> (c > 0), n >> (c > 0))).astype(np.int16) for c in range(3)]
+            b.add_cu(x, y, log2, 0, [0] * 4, 0, qy, qcb, qcr, [], pcm=True, pcm_samples=smp)
+            return
         nxn = log2 == 3 and rng.random() < 0.41
         modes = [mode() for _ in range(4 if nxn else 1)] + [0] * (0 if nxn else 3)
         mc = chroma_mode(modes[0])
@@ -164,9 +178,11 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
         else:
             typ, ab, sg, band, eo = [0, 0, 0], None, None, (0, 0, 0), (0, 0, 0)
         s = int(slice_of_ts[ts])
+        on, bo, to = slice_dbk[s]
         b.add_ctu(int(rs), slice_addr=int(slice_addr_ts[ts]), tile_id=int(tile[rs]), lf_across_slices=slice_lf[s],
-                  sao_type=typ, sao_abs=ab, sao_sign=sg, sao_band=band, sao_eo=eo)
-    return b.finish(meta={"seed": seed, "perf": perf, "tiles": tiles, "slices": n_slices})
+                  sao_type=typ, sao_abs=ab, sao_sign=sg, sao_band=band, sao_eo=eo,
+                  deblocking=on, beta_offset_div2=bo, tc_offset_div2=to)
+    return b.finish(meta={"seed": seed, "perf": perf, "tiles": tiles, "slices": n_slices, "deblocking": deblocking})
 
 
 def c2_picture(seed=267):

@@ -185,3 +185,54 @@ def test_component_major_tb_order(recon_mod):
     _check(recon_mod, params, pics, "component-major")
     params, sp = frontend.pictures_from_frontend_npz(os.path.join(GOLDEN, "sanity_frontend.npz"))
     _check(recon_mod, params, [_component_major(sp[0])], "sanity-component-major")
+
+
+# ---------------------------------------------------------------------------------
+# in-loop filters: deblocking (8.7.2) + SAO fused in loopfilter_kernel
+# ---------------------------------------------------------------------------------
+
+def _check_c(recon_mod, params, pics, label=""):
+    """Like _check, against the C oracle twin (equal to the Python one: tests/test_deblock.py)."""
+    from oracle import c_oracle
+    with recon_mod.ReconContext(params) as ctx:
+        outs, recs = ctx.decode(pics, with_recon=True)
+    ref = c_oracle.decode(params, pics, threads=8)
+    for i in range(len(pics)):
+        for c in range(3):
+            np.testing.assert_array_equal(recs[i][c], ref[i][0][c], err_msg="%s pic %d recon c%d" % (label, i, c))
+            np.testing.assert_array_equal(outs[i][c], ref[i][1][c], err_msg="%s pic %d out c%d" % (label, i, c))
+
+
+@pytest.mark.parametrize("ctb_log2,w,h,tiles,slices,lf_tiles,sao", [
+    (6, 352, 288, (1, 1), 1, 1, True), (5, 264, 200, (3, 2), 4, 0, True), (5, 264, 200, (3, 2), 4, 1, False),
+    (4, 72, 40, (1, 1), 3, 1, True), (6, 136, 72, (2, 1), 2, 1, True), (4, 200, 136, (2, 2), 5, 0, False)])
+def test_deblocking_synthetic(recon_mod, ctb_log2, w, h, tiles, slices, lf_tiles, sao):
+    params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2, loop_filter_across_tiles=lf_tiles,
+                           sample_adaptive_offset=int(sao), pps_cb_qp_offset=(w % 7) - 3, pps_cr_qp_offset=3 - (h % 7))
+    pics = [synth.make_picture(params, 1300 + 7 * s + ctb_log2, perf=False, tiles=tiles, n_slices=slices,
+                               lf_across_slices=None, deblocking="random", bypass_rate=0.04, pcm_rate=0.03, sao=sao)
+            for s in range(3)]
+    _check(recon_mod, params, pics, "dbk")
+
+
+def test_deblocking_1080p(recon_mod):
+    params = R.make_params(pic_width=1920, pic_height=1080)
+    pics = [synth.make_picture(params, 265 + 4 + s, perf=True, deblocking=True) for s in range(2)]
+    _check_c(recon_mod, params, pics, "dbk-1080p")
+
+
+def test_deblocking_4k_tiles(recon_mod):
+    params = R.make_params(pic_width=3840, pic_height=2160, loop_filter_across_tiles=1)
+    pics = [synth.make_picture(params, 4000, perf=True, tiles=(2, 2), deblocking="random")]
+    _check_c(recon_mod, params, pics, "dbk-4k")
+
+
+@pytest.mark.parametrize("kernel", ["window", "direct"])
+def test_sao_kernels_agree(recon_mod, monkeypatch, kernel):
+    """SAO-only batches: the windowed loop-filter kernel and the direct SAO kernel."""
+    monkeypatch.setenv("P265R_SAO_KERNEL", kernel)
+    for ctb_log2, w, h in ((6, 200, 136), (5, 264, 200), (4, 72, 40)):
+        params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2, loop_filter_across_tiles=0)
+        pics = [synth.make_picture(params, 1700 + s, perf=False, tiles=(2, 1), n_slices=3, lf_across_slices=None,
+                                   bypass_rate=0.05) for s in range(2)]
+        _check_c(recon_mod, params, pics, "sao-%s" % kernel)
