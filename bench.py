@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--unique", type=int, default=4, help="distinct synthetic pictures per rank (replicated)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--deblocking", action="store_true",
+                    help="deblocking on in every slice (real-stream config; SURVEY §8(d) defines the bench without it)")
     return ap.parse_args()
 
 
@@ -79,6 +81,37 @@ def algorithmic_bytes(pics):
         resid += 4 * c + 8 * int(((p.tbs["flags"] & 1) != 0).sum())
         sao += 2 * s + 32 * nctu
     return tot, intra, resid, sao
+
+
+def cpu_baseline_python(procs, timeout_s=600):
+    """The pure-Python restatement (oracle/py_baseline.py) in a child process that never
+    touches the GPU: one 1080p picture per worker, ``procs`` workers."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-m", "oracle.py_baseline", "--procs", str(procs)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout_s)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode or not lines:
+        return {"error": (r.stderr or "no output")[-300:]}
+    return json.loads(lines[-1])
+
+
+def hbm_copy_gbs(device, nbytes=4 << 30, reps=10):
+    """Achievable HBM bandwidth on this box: a device-to-device copy (read + write bytes / time)."""
+    import torch
+    x = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    torch.cuda.synchronize(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / reps
+    del x, y
+    torch.cuda.empty_cache()
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
 def cpu_baseline(params, uniq, budget_s):
@@ -106,12 +139,17 @@ def main():
     from p265_amd import dist, recon, synth
     from p265_amd import records as R
 
+    # pure-Python CPU baseline first, in a child process, before this process touches the GPU
+    py_base = None
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not a.no_cpu_baseline:
+        py_base = cpu_baseline_python(max(1, min(16, os.cpu_count() or 1)))
     rank, world, local = dist.init("nccl")
     params = R.make_params(pic_width=1920, pic_height=1080)
     params = dist.broadcast_params(params)                  # RCCL broadcast of the SPS/PPS POD
 
     t0 = time.time()
-    uniq = [synth.make_picture(params, 268 + 1000 * rank + i, perf=True) for i in range(a.unique)]
+    uniq = [synth.make_picture(params, 268 + 1000 * rank + i, perf=True, deblocking=a.deblocking)
+            for i in range(a.unique)]
     for p in uniq:
         p.meta["samples"] = 1920 * 1080 * 3 // 2
     pics = [uniq[i % a.unique] for i in range(a.frames)]
@@ -153,7 +191,8 @@ def main():
         "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8 samples / int16 coefficients (integer)",
         "data": "synthetic: seeded all-intra records with sanity.bin statistics (p265_amd/synth.py)",
-        "config": {"workload": "C3/C4: 1080p all-intra + SAO, %d pictures per GPU per step (%d distinct)" % (a.frames, a.unique),
+        "config": {"workload": "C3/C4: 1080p all-intra + %sSAO, %d pictures per GPU per step (%d distinct)"
+                               % ("deblocking + " if a.deblocking else "", a.frames, a.unique),
                    "pictures_per_gpu": a.frames, "ctus_per_picture": n_ctu, "ctb": 64,
                    "parallelism": "picture-sharded x%d" % world},
         "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel", "achieved": round(achieved, 2),
@@ -167,8 +206,11 @@ def main():
                       "whole_path_algorithmic": round(tot_b / (elapsed / a.steps) / 1e9, 2)},
         "setup_s": round(gen_s, 1),
     }
+    if rank == 0:
+        out["roofline"]["achievable_copy_gbs"] = hbm_copy_gbs(local)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(params, uniq, a.cpu_baseline_seconds)
+        out["cpu_baseline"] = py_base
+        out["cpu_baseline_c"] = cpu_baseline(params, uniq, a.cpu_baseline_seconds)
     batch.free()
     ctx.close()
     if rank == 0:
