@@ -56,7 +56,7 @@ struct Geo {                    // batch-uniform geometry
 __constant__ int8_t  c_angle[35];
 __constant__ int16_t c_inv_angle[35];
 
-__device__ __forceinline__ int morton4(int x, int y) {      // 4-bit x, y -> 8-bit z-order
+__host__ __device__ __forceinline__ int morton4(int x, int y) {      // 4-bit x, y -> 8-bit z-order
     x = (x | (x << 2)) & 0x33; x = (x | (x << 1)) & 0x55;
     y = (y | (y << 2)) & 0x33; y = (y | (y << 1)) & 0x55;
     return x | (y << 1);
@@ -92,7 +92,7 @@ __device__ __forceinline__ bool nb_available(int xl, int yl, int xc, int yc, int
     return morton4(xl >> 2, yl >> 2) < morton4(xc >> 2, yc >> 2);
 }
 
-__device__ __forceinline__ bool nb_available_wh(int xl, int yl, int xc, int yc, int x0, int y0,
+__host__ __device__ __forceinline__ bool nb_available_wh(int xl, int yl, int xc, int yc, int x0, int y0,
                                                 int w, int h, int ctb, unsigned flags) {
     if (x0 + xl >= w || y0 + yl >= h) return false;
     if (yl < 0) {
@@ -104,6 +104,41 @@ __device__ __forceinline__ bool nb_available_wh(int xl, int yl, int xc, int yc, 
     if (xl < 0) return (yl < ctb) && (flags & 1u);
     if (xl >= ctb || yl >= ctb) return false;
     return morton4(xl >> 2, yl >> 2) < morton4(xc >> 2, yc >> 2);
+}
+
+// Availability (6.4.1) of the 2L+1 reference units of an intra TB in the linear order of
+// 8.4.4.2.2 (bit u; unit = 4 luma samples: left units u < L bottom-up, corner u = L, top
+// units u > L left to right), for a TB of n x n samples of component c at component
+// position (xr, yr) inside the CTB whose luma origin is (x0, y0).  flags: neighbouring
+// CTUs usable (bit0 L, bit1 T, bit2 TL, bit3 TR; same slice and tile).  Equal to
+// nb_available_wh() unit by unit (tools/avail_check.hip): the bottom-left units lie in one
+// aligned block, so one z-order comparison decides them all, likewise the top-right
+// units; only the picture's bottom / right edges cut them unit by unit.
+__host__ __device__ __forceinline__ unsigned long long ref_avail_mask(int c, int xr, int yr, int n, int x0, int y0,
+                                                                      int w, int h, int ctb, unsigned flags) {
+    const int sub = c ? 1 : 0;
+    const int xc = xr << sub, yc = yr << sub, nl = n << sub;      // luma, CTB-relative
+    const int L = (2 * n) >> (c ? 1 : 2);                         // units per side
+    const int half = L >> 1;
+    const int zc = morton4(xc >> 2, yc >> 2);
+    const bool left = xc > 0 || (flags & 1u);
+    const bool bl = yc + nl < ctb && (xc == 0 ? (flags & 1u) != 0 : morton4((xc - 1) >> 2, (yc + nl) >> 2) < zc);
+    const bool corner = xc > 0 ? (yc > 0 ? true : (flags & 2u) != 0) : (yc > 0 ? (flags & 1u) != 0 : (flags & 4u) != 0);
+    const bool top = yc > 0 || (flags & 2u);
+    const bool tr = xc + nl < ctb ? (yc > 0 ? morton4((xc + nl) >> 2, (yc - 1) >> 2) < zc : (flags & 2u) != 0)
+                                  : (yc == 0 && (flags & 8u));
+    auto bits = [](int lo, int hi) -> unsigned long long {        // bits [lo, hi)
+        return hi <= lo ? 0ull : (((hi >= 64) ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull));
+    };
+    const int u_min = max(0, (y0 + yc + 2 * nl - h) >> 2);        // units below the picture: u < u_min
+    const int j_max = (w - x0 - xc) >> 2;                          // top units inside the picture: j < j_max
+    unsigned long long m = 0;
+    if (bl) m |= bits(u_min, half);
+    if (left) m |= bits(half, L);
+    if (corner) m |= 1ull << L;
+    if (top) m |= bits(L + 1, L + 1 + half);
+    if (tr) m |= bits(L + 1 + half, L + 1 + min(L, j_max));
+    return m;
 }
 
 __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict__ pics,

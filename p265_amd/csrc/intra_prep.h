@@ -85,18 +85,8 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const uint32_t cm = c == 0 ? 0u : (pair ? 3u : (uint32_t)c);
             const int mode = rec.pred_mode;
             // ---- availability per reference unit, linear order (8.4.4.2.2) -----------------
-            const int us_log = c ? 1 : 2;
-            const int L = (2 * n) >> us_log;
-            const int xc = xr << sub, yc = yr << sub;
-            unsigned long long m = 0;
-            for (int u = 0; u <= 2 * L; ++u) {
-                int dx, dy;
-                if (u < L) { dx = -1; dy = 2 * n - 1 - (u << us_log); }
-                else if (u == L) { dx = -1; dy = -1; }
-                else { dx = (u - L - 1) << us_log; dy = -1; }
-                if (nb_available_wh((xr + dx) << sub, (yr + dy) << sub, xc, yc, x0, y0, g.w, g.h, ctb, flags))
-                    m |= 1ull << u;
-            }
+            const int L = (2 * n) >> (c ? 1 : 2);
+            const unsigned long long m = ref_avail_mask(c, xr, yr, n, x0, y0, g.w, g.h, ctb, flags);
             const unsigned long long full = (1ull << (2 * L + 1)) - 1ull;
             // ---- filtering decision (8.4.4.2.3), luma only in 4:2:0 ---------------------------
             uint32_t filt = 0;

@@ -133,6 +133,21 @@ __device__ __forceinline__ void dbk_chroma_line(int& p0, int p1, int& q0, int q1
     if (!noq) q0 = nq0;
 }
 
+// packed unsigned 16-bit ops (two samples per dword); inline asm keeps them packed (the
+// compiler otherwise splits clamped / min forms into per-element compares)
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+    uint32_t r; asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
+    uint32_t r; asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b) {       // max(a - b, 0)
+    uint32_t r; asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    uint32_t r; asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+
 __device__ __forceinline__ int byte_of(uint32_t w, int b) { return (int)((w >> (8 * b)) & 0xffu); }
 __device__ __forceinline__ uint32_t set_byte(uint32_t w, int b, int v) {
     return (w & ~(0xffu << (8 * b))) | ((uint32_t)v << (8 * b));
@@ -147,8 +162,14 @@ struct LfCtu {                  // the fields of a neighbouring CTU record the f
 
 template <int CTBL> struct LfShape {
     static constexpr int S = 1 << CTBL, SC = S / 2;
-    static constexpr int RL = S + 8, RC = SC + 8;          // window sizes (halo 4)
-    static constexpr int WL = RL / 4, WC = RC / 4;         // dwords per window row
+    static constexpr int RL = S + 8, RC = SC + 8;          // window rows (halo 4) and used columns
+    static constexpr int WL = RL / 4, WC = RC / 4;         // used dwords per window row (4-sample segments)
+    // physical window rows start GL / GC samples left of the CTB (load granule: 16 B, 8 B for
+    // 8-wide chroma CTBs) so every global load is one aligned 16-B (8-B) access
+    static constexpr int GL = 16, GC = SC >= 16 ? 16 : 8;
+    static constexpr int PL = (GL + S + 4 + GL - 1) / GL * GL / 4;     // dwords per physical row
+    static constexpr int PC = (GC + SC + 4 + GC - 1) / GC * GC / 4;
+    static constexpr int DXL = (GL - 4) / 4, DXC = (GC - 4) / 4;      // dword of sample x0 - 4
     static constexpr int NB = S / 8 + 2;                   // 8x8 luma blocks per window row (map)
     static constexpr int UL = 16, UC = SC < 16 ? SC : 16;  // SAO unit widths (samples)
     static constexpr int N_SAO = S * (S / UL) + 2 * SC * (SC / UC);
@@ -159,20 +180,38 @@ template <int CTBL> struct LfShape {
 };
 
 // grid (CTUs, pictures); DBK: deblock the window first (else the window is the SAO input as is)
+// XCD-aware block order: hardware block b runs on XCD b % 8 (observed round-robin,
+// MI355X_MICROARCH.md); logical unit (picture, CTB) = (b % 8) * per + b / 8, so each XCD
+// walks one contiguous raster range and the halo rows / columns its windows share with
+// the neighbouring CTBs are read from its own L2.
+__device__ __forceinline__ int xcd_unit(int b, int n_units) {
+    const int per = (n_units + 7) >> 3;
+    return (b & 7) * per + (b >> 3);
+}
+
+// grid (8 * ceil(CTUs * pictures / 8)); DBK: deblock the window first (else the window is
+// the SAO input as is)
 template <int CTBL, bool DBK>
 __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(const DevPic* __restrict__ pics, Geo g,
-                                                                          int sao_on) {
+                                                                          int sao_on, int n_pics) {
     using SH = LfShape<CTBL>;
     constexpr int S = SH::S, SC = SH::SC, WL = SH::WL, WC = SH::WC, NB = SH::NB;
-    __shared__ uint32_t s_l[SH::RL * WL];
-    __shared__ uint32_t s_c[2][SH::RC * WC];
+    constexpr int PL = SH::PL, PC = SH::PC;
+    __shared__ __attribute__((aligned(16))) uint32_t s_lphys[SH::RL * PL];
+    __shared__ __attribute__((aligned(16))) uint32_t s_cphys[2][SH::RC * PC];
+    // logical windows: row r, dword d = samples (x0 - 4 + 4d .. +3, y0 - 4 + r)
+    uint32_t* const s_l = s_lphys + SH::DXL;
+    auto s_cw = [&](int c) -> uint32_t* { return (c ? s_cphys[1] : s_cphys[0]) + SH::DXC; };
     __shared__ uint8_t s_map[NB * NB];
     __shared__ uint8_t s_nf[NB * NB];
     __shared__ LfCtu s_ctu[9];
     __shared__ uint32_t s_allow;
 
-    const int rs = blockIdx.x;
-    const DevPic* P = pics + blockIdx.y;
+    const int n_ctus = g.wc * g.hc;
+    const int unit = xcd_unit(blockIdx.x, n_ctus * n_pics);
+    if (unit >= n_ctus * n_pics) return;                         // whole workgroup: before any barrier
+    const int pic = unit / n_ctus, rs = unit - pic * n_ctus;
+    const DevPic* P = pics + pic;
     const p265r_ctu* ctus = P->ctus;
     const int rx = rs % g.wc, ry = rs / g.wc;
     const int x0 = rx * S, y0 = ry * S, xc0 = x0 >> 1, yc0 = y0 >> 1;
@@ -204,17 +243,35 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
         s_nf[i] = in && P->nofilter ? P->nofilter[o] : 0;
     }
     {
+        // sample windows: aligned 16-B (8-B) loads; bytes right of the picture edge come from
+        // the row padding (stride >= 64-aligned width) and are never used
+        constexpr int QL = PL / 4;                                 // uint4 per luma row
         const uint8_t* src = P->rec[0];
         const int st = g.stride[0];
-        for (int i = tid; i < SH::RL * WL; i += T) {
-            const int gy = y0 - 4 + i / WL, gx = x0 - 4 + 4 * (i % WL);
-            s_l[i] = (gy >= 0 && gy < g.h && gx >= 0 && gx < g.w) ? *reinterpret_cast<const uint32_t*>(src + (size_t)gy * st + gx) : 0u;
+        for (int i = tid; i < SH::RL * QL; i += T) {
+            const int r = i / QL, q = i - r * QL;
+            const int gy = y0 - 4 + r, gx = x0 - SH::GL + 16 * q;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (gy >= 0 && gy < g.h && gx >= 0 && gx < g.w) v = *reinterpret_cast<const uint4*>(src + (size_t)gy * st + gx);
+            *reinterpret_cast<uint4*>(&s_lphys[r * PL + 4 * q]) = v;
         }
-        for (int i = tid; i < 2 * SH::RC * WC; i += T) {
-            const int c = i >= SH::RC * WC, k = i - c * SH::RC * WC;
-            const int gy = yc0 - 4 + k / WC, gx = xc0 - 4 + 4 * (k % WC);
-            s_c[c][k] = (gy >= 0 && gy < g.ch && gx >= 0 && gx < g.cw)
-                            ? *reinterpret_cast<const uint32_t*>(P->rec[1 + c] + (size_t)gy * g.stride[1] + gx) : 0u;
+        constexpr int GCW = SH::GC / 4;                            // dwords per chroma granule
+        constexpr int QC = PC / GCW;
+        for (int i = tid; i < 2 * SH::RC * QC; i += T) {
+            const int c = i >= SH::RC * QC, k = i - c * SH::RC * QC;
+            const int r = k / QC, q = k - r * QC;
+            const int gy = yc0 - 4 + r, gx = xc0 - SH::GC + SH::GC * q;
+            const bool in = gy >= 0 && gy < g.ch && gx >= 0 && gx < g.cw;
+            const uint8_t* p = P->rec[1 + c] + (size_t)gy * g.stride[1] + gx;
+            if constexpr (GCW == 4) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (in) v = *reinterpret_cast<const uint4*>(p);
+                *reinterpret_cast<uint4*>(&s_cphys[c][r * PC + 4 * q]) = v;
+            } else {
+                uint2 v = make_uint2(0, 0);
+                if (in) v = *reinterpret_cast<const uint2*>(p);
+                *reinterpret_cast<uint2*>(&s_cphys[c][r * PC + 2 * q]) = v;
+            }
         }
     }
     __syncthreads();
@@ -252,14 +309,14 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
                     if (!dir) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            const uint32_t lo = s_l[(4 * j + k) * WL + 2 * i], hi = s_l[(4 * j + k) * WL + 2 * i + 1];
+                            const uint32_t lo = s_l[(4 * j + k) * PL + 2 * i], hi = s_l[(4 * j + k) * PL + 2 * i + 1];
 #pragma unroll
                             for (int a = 0; a < 4; ++a) { Pm[a][k] = byte_of(lo, 3 - a); Qm[a][k] = byte_of(hi, a); }
                         }
                     } else {
 #pragma unroll
                         for (int a = 0; a < 4; ++a) {
-                            const uint32_t wp = s_l[(8 * i + 3 - a) * WL + j], wq = s_l[(8 * i + 4 + a) * WL + j];
+                            const uint32_t wp = s_l[(8 * i + 3 - a) * PL + j], wq = s_l[(8 * i + 4 + a) * PL + j];
 #pragma unroll
                             for (int k = 0; k < 4; ++k) { Pm[a][k] = byte_of(wp, k); Qm[a][k] = byte_of(wq, k); }
                         }
@@ -272,8 +329,8 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
                             uint32_t lo = 0, hi = 0;
 #pragma unroll
                             for (int a = 0; a < 4; ++a) { lo |= (uint32_t)Pm[3 - a][k] << (8 * a); hi |= (uint32_t)Qm[a][k] << (8 * a); }
-                            s_l[(4 * j + k) * WL + 2 * i] = lo;
-                            s_l[(4 * j + k) * WL + 2 * i + 1] = hi;
+                            s_l[(4 * j + k) * PL + 2 * i] = lo;
+                            s_l[(4 * j + k) * PL + 2 * i + 1] = hi;
                         }
                     } else {
 #pragma unroll
@@ -281,8 +338,8 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
                             uint32_t wp = 0, wq = 0;
 #pragma unroll
                             for (int k = 0; k < 4; ++k) { wp |= (uint32_t)Pm[a][k] << (8 * k); wq |= (uint32_t)Qm[a][k] << (8 * k); }
-                            s_l[(8 * i + 3 - a) * WL + j] = wp;
-                            s_l[(8 * i + 4 + a) * WL + j] = wq;
+                            s_l[(8 * i + 3 - a) * PL + j] = wp;
+                            s_l[(8 * i + 4 + a) * PL + j] = wq;
                         }
                     }
                 } else {
@@ -303,19 +360,19 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
                     const int qpi = (((mq & DBK_QP) + (s_map[bp] & DBK_QP) + 1) >> 1) + g.cqp[c];
                     const int tc = c_tc_table[min(max(qpc_table(qpi) + 2 + 2 * nib4(offs >> 4), 0), 53)];
                     const bool nop = s_nf[bp] != 0, noq = s_nf[bq] != 0;
-                    uint32_t* w = s_c[c];
+                    uint32_t* w = s_cw(c);
                     if (!dir) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            uint32_t lo = w[(4 * j + k) * WC + 2 * i], hi = w[(4 * j + k) * WC + 2 * i + 1];
+                            uint32_t lo = w[(4 * j + k) * PC + 2 * i], hi = w[(4 * j + k) * PC + 2 * i + 1];
                             int p0 = byte_of(lo, 3), q0 = byte_of(hi, 0);
                             dbk_chroma_line(p0, byte_of(lo, 2), q0, byte_of(hi, 1), tc, nop, noq);
-                            w[(4 * j + k) * WC + 2 * i] = set_byte(lo, 3, p0);
-                            w[(4 * j + k) * WC + 2 * i + 1] = set_byte(hi, 0, q0);
+                            w[(4 * j + k) * PC + 2 * i] = set_byte(lo, 3, p0);
+                            w[(4 * j + k) * PC + 2 * i + 1] = set_byte(hi, 0, q0);
                         }
                     } else {
-                        const uint32_t w1 = w[(8 * i + 2) * WC + j], w4 = w[(8 * i + 5) * WC + j];
-                        uint32_t w2 = w[(8 * i + 3) * WC + j], w3 = w[(8 * i + 4) * WC + j];
+                        const uint32_t w1 = w[(8 * i + 2) * PC + j], w4 = w[(8 * i + 5) * PC + j];
+                        uint32_t w2 = w[(8 * i + 3) * PC + j], w3 = w[(8 * i + 4) * PC + j];
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
                             int p0 = byte_of(w2, k), q0 = byte_of(w3, k);
@@ -323,8 +380,8 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
                             w2 = set_byte(w2, k, p0);
                             w3 = set_byte(w3, k, q0);
                         }
-                        w[(8 * i + 3) * WC + j] = w2;
-                        w[(8 * i + 4) * WC + j] = w3;
+                        w[(8 * i + 3) * PC + j] = w2;
+                        w[(8 * i + 4) * PC + j] = w3;
                     }
                 }
             }
@@ -349,8 +406,8 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
     const int xb = c ? xc0 : x0, yb = c ? yc0 : y0;
     const int X = xb + col, Y = yb + row;
     if (X >= W || Y >= H) return;
-    const uint32_t* win = c ? s_c[c - 1] : s_l;
-    const int wst = c ? WC : WL;
+    const uint32_t* win = c ? s_cw(c - 1) : s_l;
+    const int wst = c ? PC : PL;
     // window dword (r, d) holds samples (xb - 4 + 4d .. +3, yb - 4 + r)
     const int wr = row + 4, wd = col / 4 + 1;
     uint32_t cur[4], res[4];
@@ -360,66 +417,109 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
     for (int q = 0; q < 4; ++q) res[q] = cur[q];
     const int typ = sao_on ? me.sao_type[c] : 0;
     if (typ != 0) {
-        uint32_t keep = 0;
-        for (int i = 0; i < U; i += 4) {                 // 4 samples never straddle an 8x8 luma block
-            const int lx = (X + i) << sub, ly = Y << sub;
-            if (s_nf[((ly >> 3) - (y0 >> 3) + 1) * NB + (lx >> 3) - (x0 >> 3) + 1]) keep |= 0xfu << i;
-        }
-        const int o1 = me.sao_offset[c][0], o2 = me.sao_offset[c][1];
-        const int o3 = me.sao_offset[c][2], o4 = me.sao_offset[c][3];
-        auto offv = [&](int i) { return i == 1 ? o1 : i == 2 ? o2 : i == 3 ? o3 : i == 4 ? o4 : 0; };
+        // packed byte arithmetic, 4 samples per dword (SWAR): per sample a table index
+        // (edgeIdx or band slot) is built in a byte, the offsets are looked up 4 at a time
+        // with v_perm_b32 from 8-byte tables, and v + offset is clipped in 16-bit lanes
         const int cls = me.sao_class[c];
-        if (typ == 1) {
+        int tab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (typ == 2) {        // raw e = 2 + sgn(v - a) + sgn(v - b): edgeIdx 1, 2, 0, 3, 4
+            tab[0] = me.sao_offset[c][0]; tab[1] = me.sao_offset[c][1];
+            tab[3] = me.sao_offset[c][2]; tab[4] = me.sao_offset[c][3];
+        } else {               // slot 1..4 = bands sao_band_position + 0..3, slot 0 = no offset
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if (i >= U) break;
-                const int v = byte_of(cur[i >> 2], i & 3);
-                const int bi = ((v >> 3) - cls) & 31;
-                int r = v;
-                if (bi < 4) r = min(max(v + offv(bi + 1), 0), 255);
-                if ((keep >> i) & 1u) r = v;
-                res[i >> 2] = set_byte(res[i >> 2], i & 3, r);
+            for (int k = 0; k < 4; ++k) tab[k + 1] = me.sao_offset[c][k];
+        }
+        uint32_t tp_lo = 0, tp_hi = 0, tn_lo = 0, tn_hi = 0;       // max(off, 0) / max(-off, 0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tp_lo |= (uint32_t)max(tab[k], 0) << (8 * k);
+            tn_lo |= (uint32_t)max(-tab[k], 0) << (8 * k);
+            tp_hi |= (uint32_t)max(tab[k + 4], 0) << (8 * k);
+            tn_hi |= (uint32_t)max(-tab[k + 4], 0) << (8 * k);
+        }
+        // which samples of the unit may be changed: neighbours available (EO), not PCM/bypass
+        uint32_t okm[4];
+        const bool has_l = X > 0, has_u = Y > 0, has_d = Y + 1 < H, right_in = X + U < W;
+        const int ru = Y == yb ? 0 : 1, rd = Y == yb + cs - 1 ? 2 : 1;
+        const int cl = X == xb ? 0 : 1, cr = X + U == xb + cs ? 2 : 1;
+        auto rok = [&](int rr, int cc) { return ((allow >> (rr * 3 + cc)) & 1u) != 0; };
+        bool mid = true, first = true, last = true;
+        if (typ == 2) {
+            const bool vert = has_u && has_d;
+            if (cls == 0) { first = has_l && rok(1, cl); last = right_in && rok(1, cr); }
+            else if (cls == 1) { mid = first = last = vert && rok(ru, 1) && rok(rd, 1); }
+            else if (cls == 2) {
+                mid = vert && rok(ru, 1) && rok(rd, 1);
+                first = vert && has_l && rok(ru, cl) && rok(rd, 1);
+                last = vert && right_in && rok(ru, 1) && rok(rd, cr);
+            } else {
+                mid = vert && rok(ru, 1) && rok(rd, 1);
+                first = vert && has_l && rok(ru, 1) && rok(rd, cl);
+                last = vert && right_in && rok(ru, cr) && rok(rd, 1);
+            }
+        }
+        const int ilast = min(U, W - X) - 1;                 // last sample inside the picture
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t m = mid ? 0xffffffffu : 0u;
+            if (q == 0) m = first ? (m | 0xffu) : (m & ~0xffu);
+            if (q == (ilast >> 2)) {
+                const uint32_t b = 0xffu << (8 * (ilast & 3));
+                m = last ? (m | b) : (m & ~b);
+            }
+            // 4 samples never straddle an 8x8 luma block
+            const int lx = (X + 4 * q) << sub, ly = Y << sub;
+            if (s_nf[((ly >> 3) - (y0 >> 3) + 1) * NB + (lx >> 3) - (x0 >> 3) + 1]) m = 0;
+            okm[q] = m;
+        }
+        auto split_lo = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0c020c00u); };   // bytes 0, 2
+        auto split_hi = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0c030c01u); };   // bytes 1, 3
+        auto join = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x06020400u); };
+        // v + table[sel] clipped to [0, 255], 4 samples
+        auto apply = [&](uint32_t v, uint32_t sel) {
+            const uint32_t pos = __builtin_amdgcn_perm(tp_hi, tp_lo, sel);
+            const uint32_t neg = __builtin_amdgcn_perm(tn_hi, tn_lo, sel);
+            const uint32_t m255 = 0x00ff00ffu;
+            const uint32_t rl = pk_min_u16(pk_subsat_u16(pk_add_u16(split_lo(v), split_lo(pos)), split_lo(neg)), m255);
+            const uint32_t rh = pk_min_u16(pk_subsat_u16(pk_add_u16(split_hi(v), split_hi(pos)), split_hi(neg)), m255);
+            return join(rl, rh);
+        };
+        if (typ == 1) {
+            const uint32_t badd = (uint32_t)((32 - cls) & 31) * 0x01010101u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q >= NW) break;
+                const uint32_t k = (((cur[q] >> 3) & 0x1f1f1f1fu) + badd) & 0x1f1f1f1fu;
+                const uint32_t big = (((k & 0x1c1c1c1cu) + 0x7f7f7f7fu) & 0x80808080u) >> 7;
+                const uint32_t sel = (k + 0x01010101u) & ~((big << 8) - big);
+                res[q] = (apply(cur[q], sel) & okm[q]) | (cur[q] & ~okm[q]);
             }
         } else {
-            const int ax = cls == 1 ? 0 : (cls == 3 ? 1 : -1);
-            const int ay = cls == 0 ? 0 : -1;
-            const bool has_l = X > 0, has_u = Y > 0, has_d = Y + 1 < H;
-            const int ru = Y == yb ? 0 : 1, rd = Y == yb + cs - 1 ? 2 : 1;
-            const int cl = X == xb ? 0 : 1, cr = X + U == xb + cs ? 2 : 1;
-            auto region_ok = [&](int rr, int cc) { return (allow >> (rr * 3 + cc)) & 1u; };
-            // sample at unit column j (-1 .. U) of window row r
-            auto at = [&](int r, int j) {
-                const int d = wd + ((j + 4) >> 2) - 1;
-                return byte_of(win[r * wst + d], (j + 4) & 3);
+            // rows above / below with one dword either side (window dwords wd-1 .. wd+NW)
+            uint32_t up[6], mi[6], dn[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const bool in = q <= NW + 1;
+                mi[q] = in ? win[wr * wst + wd - 1 + q] : 0u;
+                up[q] = in ? win[(wr - 1) * wst + wd - 1 + q] : 0u;
+                dn[q] = in ? win[(wr + 1) * wst + wd - 1 + q] : 0u;
+            }
+            // 2 + sgn(v - a) + sgn(v - b) in unsigned 16-bit lanes: [v > a] = min(sat(v - a), 1)
+            auto gt = [&](uint32_t v, uint32_t a) { return pk_min_u16(pk_subsat_u16(v, a), 0x00010001u); };
+            auto edge = [&](uint32_t v, uint32_t a, uint32_t b) {
+                return pk_sub_u16(pk_add_u16(pk_add_u16(gt(v, a), gt(v, b)), 0x00020002u), pk_add_u16(gt(a, v), gt(b, v)));
             };
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if (i >= U) break;
-                const int v = byte_of(cur[i >> 2], i & 3);
-                const int ja = i + ax, jb = i - ax;
-                const int ca = ja < 0 ? cl : (ja >= U ? cr : 1);
-                const int cb = jb < 0 ? cl : (jb >= U ? cr : 1);
-                const bool xa_in = ja < 0 ? has_l : X + ja < W;
-                const bool xb_in = jb < 0 ? has_l : X + jb < W;
-                bool ok, okb;
-                int a, b;
-                if (ay == 0) {
-                    ok = xa_in && region_ok(1, ca);
-                    okb = xb_in && region_ok(1, cb);
-                    a = at(wr, ja); b = at(wr, jb);
-                } else {
-                    ok = has_u && xa_in && region_ok(ru, ca);
-                    okb = has_d && xb_in && region_ok(rd, cb);
-                    a = at(wr - 1, ja); b = at(wr + 1, jb);
-                }
-                int r = v;
-                if (ok && okb) {
-                    int ei = 2 + sgn(v - a) + sgn(v - b);
-                    ei = ei == 2 ? 0 : (ei < 2 ? ei + 1 : ei);
-                    r = min(max(v + offv(ei), 0), 255);
-                }
-                if ((keep >> i) & 1u) r = v;
-                res[i >> 2] = set_byte(res[i >> 2], i & 3, r);
+            for (int q = 0; q < 4; ++q) {
+                if (q >= NW) break;
+                uint32_t a, b;                                 // neighbours of the 4 samples, byte-aligned
+                if (cls == 0) { a = __builtin_amdgcn_alignbyte(mi[q + 1], mi[q], 3); b = __builtin_amdgcn_alignbyte(mi[q + 2], mi[q + 1], 1); }
+                else if (cls == 1) { a = up[q + 1]; b = dn[q + 1]; }
+                else if (cls == 2) { a = __builtin_amdgcn_alignbyte(up[q + 1], up[q], 3); b = __builtin_amdgcn_alignbyte(dn[q + 2], dn[q + 1], 1); }
+                else { a = __builtin_amdgcn_alignbyte(up[q + 2], up[q + 1], 1); b = __builtin_amdgcn_alignbyte(dn[q + 1], dn[q], 3); }
+                const uint32_t v = cur[q];
+                const uint32_t sel = join(edge(split_lo(v), split_lo(a), split_lo(b)), edge(split_hi(v), split_hi(a), split_hi(b)));
+                res[q] = (apply(v, sel) & okm[q]) | (v & ~okm[q]);
             }
         }
     }

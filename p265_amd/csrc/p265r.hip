@@ -82,7 +82,6 @@ struct p265r_ctx {
     int row_waves = 16;        // waves per workgroup of the row pipeline (4, 8 or 16)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
-    bool lf_kernel = true;     // SAO-only batches: windowed loopfilter_kernel (1) or sao_kernel (0); P265R_SAO_KERNEL
 };
 
 struct p265r_batch {
@@ -251,7 +250,6 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
-    if (const char* v = std::getenv("P265R_SAO_KERNEL")) ctx->lf_kernel = std::strcmp(v, "direct") != 0;
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 8 || w == 16) ctx->row_waves = w;
@@ -497,27 +495,18 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
-    if (b->dbk || (b->sao && ctx->lf_kernel)) {
-        const dim3 grid(ctx->n_ctus, b->n_pics);
-        const int so = b->sao ? 1 : 0;
+    if (b->dbk || b->sao) {
+        const long long units = (long long)ctx->n_ctus * b->n_pics;
+        if (units >= (1ll << 31) - 8) return P265R_ERANGE;
+        const dim3 grid((unsigned)((units + 7) / 8 * 8));
+        const int so = b->sao ? 1 : 0, np = b->n_pics;
         switch (g.ctb_log2 * 2 + (b->dbk ? 1 : 0)) {
-            case 12: loopfilter_kernel<6, false><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so); break;
-            case 13: loopfilter_kernel<6, true><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so); break;
-            case 10: loopfilter_kernel<5, false><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so); break;
-            case 11: loopfilter_kernel<5, true><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so); break;
-            case 8: loopfilter_kernel<4, false><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so); break;
-            default: loopfilter_kernel<4, true><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so); break;
-        }
-        ++tm.sao_launches;
-        HIP_TRY(hipGetLastError());
-    } else if (b->sao) {
-        const int cs = 1 << g.ctb_log2;
-        if (g.ctb_log2 >= 5) {
-            const int threads = (cs / 16) * cs + 2 * (cs / 32) * (cs / 2);
-            sao_kernel<16><<<dim3(ctx->n_ctus, b->n_pics), (threads + 63) / 64 * 64, 0, s>>>(b->d_pics, g);
-        } else {
-            const int threads = (cs / 8) * cs + 2 * (cs / 16) * (cs / 2);
-            sao_kernel<8><<<dim3(ctx->n_ctus, b->n_pics), (threads + 63) / 64 * 64, 0, s>>>(b->d_pics, g);
+            case 12: loopfilter_kernel<6, false><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
+            case 13: loopfilter_kernel<6, true><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
+            case 10: loopfilter_kernel<5, false><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
+            case 11: loopfilter_kernel<5, true><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
+            case 8: loopfilter_kernel<4, false><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
+            default: loopfilter_kernel<4, true><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
         }
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
