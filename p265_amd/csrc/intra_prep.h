@@ -22,7 +22,7 @@
 
 namespace p265r {
 
-// 32-byte job record (w5..w7 reserved, 0).
+// 32-byte job record (w6, w7 reserved, 0).
 //  w0: [0,13) LDS offset of the TB origin in WaveLds (luma yr*64+xr, chroma 4096+yr*32+xr)
 //      [13,15) log2-2  [15,17) component mask (0 luma, 1 Cb, 2 Cr, 3 Cb+Cr)  [17,23) mode
 //      23 PCM  [24,26) filter (0 none, 1 [1 2 1], 2 strong candidate)
@@ -32,12 +32,17 @@ namespace p265r {
 //  w2: availability bits 0..31 (unit u: k in [u*us, u*us+us) for u < L, corner u = L,
 //      top units u > L; us = 4 luma / 2 chroma samples, L = 2N/us)
 //  w3, w4: residual element offset of half 0 (luma / Cb) and half 1 (Cr)
+//  w5: fast-path job (intra_rows.h recon_fast): bit 31 set for luma 4x4 / 8x8 and Cb+Cr
+//      4x4 pairs, not PCM, whose available reference samples form ONE contiguous run
+//      [fa, la] of the linear order (or none): substitution (8.4.4.2.2) is then
+//      s = Clip3(fa, la, k).  fa bits 0..7, la bits 8..15.
 // (struct IntraJob: intra.h)
 
 enum : uint32_t {
     J_PCM = 1u << 23,
     J_ALL = 1u << 30,
     J_NONE = 1u << 31,
+    J5_FAST = 1u << 31,
 };
 
 __device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265r_tb& cr) {
@@ -110,7 +115,25 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             J.w[2] = (uint32_t)m;
             J.w[3] = off0;
             J.w[4] = off1;
-            J.w[5] = J.w[6] = J.w[7] = 0;
+            // fast path: one contiguous run of available units -> sample bounds [fa, la]
+            uint32_t w5 = 0;
+            const bool fast_size = (c == 0 && n <= 8) || (cm == 3u && n == 4);
+            if (fast_size && !(f0 & P265R_TB_PCM)) {
+                const int US = c ? 1 : 2;
+                if (m == 0) {
+                    w5 = J5_FAST;
+                } else {
+                    const int ulo = __ffsll((long long)m) - 1, uhi = 63 - __clzll((long long)m);
+                    const unsigned long long run = (uhi >= 63 ? ~0ull : ((2ull << uhi) - 1ull)) & ~((1ull << ulo) - 1ull);
+                    if (m == run) {
+                        auto first = [&](int u) { return u < L ? (u << US) : (u == L ? 2 * n : 2 * n + 1 + ((u - L - 1) << US)); };
+                        auto last = [&](int u) { return u < L ? ((u + 1) << US) - 1 : (u == L ? 2 * n : 2 * n + ((u - L) << US)); };
+                        w5 = J5_FAST | (uint32_t)first(ulo) | (uint32_t)last(uhi) << 8;
+                    }
+                }
+            }
+            J.w[5] = w5;
+            J.w[6] = J.w[7] = 0;
             uint4* dst = reinterpret_cast<uint4*>(jobs + slot);
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);

@@ -296,6 +296,95 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
     wave_sync();
 }
 
+// Fast job (luma 4x4 / 8x8, Cb+Cr 4x4 pair; job word 5 has J5_FAST): the available
+// reference samples form one contiguous run [fa, la] of the linear order, so 8.4.4.2.2
+// substitution is a clamp.  Lane k gathers reference sample k straight into a register;
+// prediction reads its (at most) two per-sample references with ds_bpermute, so the job
+// needs one LDS read, one bpermute round trip (two with the 8x8 [1 2 1] filter) and one
+// LDS write - no reference array in LDS and no divergent control flow.  r16 = this
+// lane's residual sample (already zero when the TB has none).
+template <int LOG2, bool PAIR>
+__device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
+                                           uint32_t w5, int r16, int lane) {
+    constexpr int n = 1 << LOG2;
+    constexpr int nn = n * n;
+    constexpr int maxv = 255;
+    const int hl = PAIR ? (lane & 31) : lane;
+    const int half = PAIR ? (lane >> 5) : 0;
+    const int ofs = (int)(w0 & 0x1fffu);
+    const int xr = PAIR ? ((ofs - 4096) & 31) : (ofs & 63);
+    const int yr = PAIR ? ((ofs - 4096) >> 5) : (ofs >> 6);
+    constexpr int ist = PAIR ? 32 : 64;
+    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + ofs + half * 1024;
+    const uint8_t* const lcol = (PAIR ? L.cleft[half] : L.yleft) + yr;
+    const int mode = (int)((w0 >> 17) & 63u);
+    const int base = half * 32;                                  // first reference lane of this half
+    // ---- gather: lane k <- reference sample Clip3(fa, la, k) -------------------------------
+    const int k = min(hl, 4 * n);
+    const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
+    const int sref = min(max(k, fa), la);
+    const uint8_t* src;
+    if (sref < 2 * n) src = xr == 0 ? lcol + (2 * n - 1 - sref) : org - 1 + (2 * n - 1 - sref) * ist;
+    else if (sref == 2 * n) src = yr == 0 ? line_top + xr - 1 : (xr == 0 ? lcol - 1 : org - ist - 1);
+    else src = yr == 0 ? line_top + xr + (sref - 2 * n - 1) : org - ist + (sref - 2 * n - 1);
+    int v = (w0 & J_NONE) ? 128 : (int)*src;
+    if (!PAIR && LOG2 == 3 && ((w0 >> 24) & 3u)) {           // [1 2 1] (8.4.4.2.3), 8x8: never strong
+        const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
+        const int vr = __builtin_amdgcn_ds_bpermute(min(k + 1, 4 * n) << 2, v);
+        if (k > 0 && k < 4 * n) v = (vl + 2 * v + vr + 2) >> 2;
+    }
+    auto ref = [&](int i) { return __builtin_amdgcn_ds_bpermute((base + i) << 2, v); };
+    auto uref = [&](int i) {                                     // reference i of this lane's half, uniform per half
+        if constexpr (PAIR) {
+            const int c0 = __builtin_amdgcn_readlane(v, i), c1 = __builtin_amdgcn_readlane(v, i + 32);
+            return half ? c1 : c0;
+        } else {
+            return __builtin_amdgcn_readlane(v, i);
+        }
+    };
+    // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------------------
+    const int sidx = hl < nn ? hl : 0;
+    const int x = sidx & (n - 1), y = sidx >> LOG2;
+    int pred;
+    if (mode == 0) {
+        const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
+        pred = ((n - 1 - x) * lft + (x + 1) * uref(3 * n + 1) + (n - 1 - y) * top + (y + 1) * uref(n - 1) + n) >> (LOG2 + 1);
+    } else if (mode == 1) {
+        const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
+        const int dc = (wave_sum<PAIR>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
+        const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
+        pred = dc;
+        if (!PAIR) {                                             // luma n < 32: edge smoothing
+            if (x == 0 && y == 0) pred = (lft + 2 * dc + top + 2) >> 2;
+            else if (y == 0) pred = (top + 3 * dc + 2) >> 2;
+            else if (x == 0) pred = (lft + 3 * dc + 2) >> 2;
+        }
+    } else {
+        const int ang = (int)(int8_t)(w1 & 0xffu);
+        const int inv = -(int)((w1 >> 8) & 0x1fffu);
+        const bool vert = mode >= 18;
+        const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
+        const int idx = ((along + 1) * ang) >> 5, fact = ((along + 1) * ang) & 31;
+        const int r0 = across + idx + 1;
+        auto refk = [&](int r) {                                 // r < 0: projected side reference (invAngle)
+            const int t = r >= 0 ? r : -((r * inv + 128) >> 8);
+            return vert ? 2 * n + t : 2 * n - t;
+        };
+        const bool bflt = !PAIR && (mode == 26 || mode == 10);
+        const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : refk(r0 + 1);
+        const int a = ref(refk(r0)), b = ref(i1);
+        pred = fact ? ((32 - fact) * a + fact * b + 16) >> 5 : a;
+        if (bflt) {
+            const int corner = uref(2 * n);
+            if (vert && x == 0) pred = clip_pel(uref(2 * n + 1) + ((b - corner) >> 1), maxv);
+            if (!vert && y == 0) pred = clip_pel(uref(2 * n - 1) + ((b - corner) >> 1), maxv);
+        }
+    }
+    const bool own = hl < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
+    if (own) org[y * ist + x] = (uint8_t)clip_pel(pred + r16, maxv);
+    wave_sync();
+}
+
 template <int W>
 __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
@@ -411,29 +500,46 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const int16_t* base = ((w0 >> (26 + h)) & 1u) ? pool : resid;
                 return reinterpret_cast<const uint4*>(base + (h ? w4 : w3) + (sidx & ~7));
             };
-            uint32_t w0n = 0, w1n = 0, w2n = 0;
+            // fast jobs (J5_FAST): one residual sample per lane (2-B load)
+            auto res_fast = [&](uint32_t w0, uint32_t w3, uint32_t w4) {
+                const bool pr = (w0 >> 15) & 3u;
+                const int lg = (int)((w0 >> 13) & 3u) + 2;
+                const int h = pr ? (lane >> 5) : 0;
+                const int hl = pr ? (lane & 31) : lane;
+                const bool cod = (w0 >> (28 + h)) & 1u;
+                const int16_t* base = ((w0 >> (26 + h)) & 1u) ? pool : resid;
+                const uint32_t o = cod ? (h ? w4 : w3) + (uint32_t)(hl < (1 << (2 * lg)) ? hl : 0) : 0u;
+                return base + o;
+            };
+            uint32_t w0n = 0, w1n = 0, w2n = 0, w5n = 0;
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-            if (nt) {
-                w0n = __builtin_amdgcn_readlane(rec0.x, 0);
-                w1n = __builtin_amdgcn_readlane(rec0.y, 0);
-                w2n = __builtin_amdgcn_readlane(rec0.z, 0);
-                const uint4* a = res_addr(w0n, __builtin_amdgcn_readlane(rec0.w, 0), __builtin_amdgcn_readlane(rec1.x, 0));
-                ra = ld16(a); rb = ld16(a + 1);
-            }
+            int r16n = 0;
+            auto fetch = [&](int l) {                            // job l of the current record block
+                w0n = __builtin_amdgcn_readlane(rec0.x, l);
+                w1n = __builtin_amdgcn_readlane(rec0.y, l);
+                w2n = __builtin_amdgcn_readlane(rec0.z, l);
+                w5n = __builtin_amdgcn_readlane(rec1.y, l);
+                const uint32_t w3 = __builtin_amdgcn_readlane(rec0.w, l), w4 = __builtin_amdgcn_readlane(rec1.x, l);
+                if (w5n & J5_FAST) {
+                    const int16_t* a = res_fast(w0n, w3, w4);
+                    r16n = *gptr(a);
+                } else {
+                    const uint4* a = res_addr(w0n, w3, w4);
+                    ra = ld16(a); rb = ld16(a + 1);
+                }
+            };
+            if (nt) fetch(0);
             for (int t = 0; t < nt; ++t) {
-                const uint32_t w0 = w0n, w1 = w1n, w2 = w2n;
+                const uint32_t w0 = w0n, w1 = w1n, w2 = w2n, w5 = w5n;
                 const uint4 ca = ra, cb = rb;
+                const int cr16 = ((w0 >> (28 + ((w0 >> 15) & 3u ? (lane >> 5) : 0))) & 1u) ? r16n : 0;
                 if (t + 1 < nt) {
                     const int l = (t + 1) & 63;
                     if (l == 0) {
                         if (t + 1 + lane < nt) { rec0 = ld16(&jl[t + 1 + lane].w[0]); rec1 = ld16(&jl[t + 1 + lane].w[4]); }
                         else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
                     }
-                    w0n = __builtin_amdgcn_readlane(rec0.x, l);
-                    w1n = __builtin_amdgcn_readlane(rec0.y, l);
-                    w2n = __builtin_amdgcn_readlane(rec0.z, l);
-                    const uint4* a = res_addr(w0n, __builtin_amdgcn_readlane(rec0.w, l), __builtin_amdgcn_readlane(rec1.x, l));
-                    ra = ld16(a); rb = ld16(a + 1);
+                    fetch(l);
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
                 // Opaque copies of the lane id and the LDS bases: keeps the compiler from
@@ -448,7 +554,13 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 WaveLds& LL = *reinterpret_cast<WaveLds*>(lds_ptr(lbase));
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
-                switch (sel) {
+                if (w5 & J5_FAST) {
+                    switch (sel) {
+                        case 0: recon_fast<2, false>(LL, tlp, w0, w1, w5, cr16, ln); break;
+                        case 1: recon_fast<3, false>(LL, tlp, w0, w1, w5, cr16, ln); break;
+                        default: recon_fast<2, true>(LL, tcp, w0, w1, w5, cr16, ln); break;
+                    }
+                } else switch (sel) {
                     case 0: recon_job<2, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
                     case 1: recon_job<3, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
                     case 2: recon_job<4, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
