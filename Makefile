@@ -18,3 +18,8 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# experiment builds: make variant V=name FLAGS="-DX=1"  ->  p265_amd/libp265r_name.so
+variant:
+	$(HIPCC) $(HIPFLAGS) $(FLAGS) -o p265_amd/libp265r_$(V).so $(SRC)
+.PHONY: variant

@@ -162,9 +162,12 @@ int  p265r_wait(p265r_ctx* ctx);
 
 /* Block until the context stream is idle. */
 int  p265r_sync(p265r_ctx* ctx);
-/* Enable (1) / disable (0) per-phase HIP-event timing; read the last run's timings. */
+/* Enable (1, which also starts a new accumulation) / disable (0) per-phase HIP-event
+ * timing of every p265r_batch_run; read the last run's timings, or the sums over all runs
+ * since enabling (runs may be queued back to back: nothing here waits per run). */
 int  p265r_set_timing(p265r_ctx* ctx, int enable);
 int  p265r_last_timings(p265r_ctx* ctx, p265r_timings* out);
+int  p265r_timings_total(p265r_ctx* ctx, p265r_timings* out, int* n_runs);
 
 /* Number of HIP devices visible (>= 0), or an error code. */
 int  p265r_device_count(void);

@@ -302,7 +302,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 // prediction reads its (at most) two per-sample references with ds_bpermute, so the job
 // needs one LDS read, one bpermute round trip (two with the 8x8 [1 2 1] filter) and one
 // LDS write - no reference array in LDS and no divergent control flow.  r16 = this
-// lane's residual sample (already zero when the TB has none).
+// lane's residual sample as loaded (ignored when the TB has none).
 template <int LOG2, bool PAIR>
 __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
                                            uint32_t w5, int r16, int lane) {
@@ -320,18 +320,26 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     const int mode = (int)((w0 >> 17) & 63u);
     const int base = half * 32;                                  // first reference lane of this half
     // ---- gather: lane k <- reference sample Clip3(fa, la, k) -------------------------------
+    // (addresses as 32-bit LDS offsets, selected without branches; NONE: all refs = 128)
     const int k = min(hl, 4 * n);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
     const int sref = min(max(k, fa), la);
-    const uint8_t* src;
-    if (sref < 2 * n) src = xr == 0 ? lcol + (2 * n - 1 - sref) : org - 1 + (2 * n - 1 - sref) * ist;
-    else if (sref == 2 * n) src = yr == 0 ? line_top + xr - 1 : (xr == 0 ? lcol - 1 : org - ist - 1);
-    else src = yr == 0 ? line_top + xr + (sref - 2 * n - 1) : org - ist + (sref - 2 * n - 1);
-    int v = (w0 & J_NONE) ? 128 : (int)*src;
+    const uint32_t orgA = (uint32_t)(uintptr_t)org, lcolA = (uint32_t)(uintptr_t)lcol;
+    const uint32_t ltA = (uint32_t)(uintptr_t)line_top + xr;
+    // left refs k < 2n at lb - k * ls, top refs k > 2n at tb + k; the corner k = 2n follows the
+    // left formula inside the CTU / left column and the top formula in the line buffer (yr = 0)
+    const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
+    const int ls = xr == 0 ? 1 : ist;
+    const uint32_t tb = (yr == 0 ? ltA : orgA - ist) - 2 * n - 1;
+    const int th = 2 * n + (yr > 0 ? 1 : 0);
+    const uint32_t sa = tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
+    const int raw = (int)*reinterpret_cast<const uint8_t*>(lds_ptr(sa));
+    int v = (w0 & J_NONE) ? 128 : raw;
     if (!PAIR && LOG2 == 3 && ((w0 >> 24) & 3u)) {           // [1 2 1] (8.4.4.2.3), 8x8: never strong
         const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
         const int vr = __builtin_amdgcn_ds_bpermute(min(k + 1, 4 * n) << 2, v);
-        if (k > 0 && k < 4 * n) v = (vl + 2 * v + vr + 2) >> 2;
+        const int f = (vl + 2 * v + vr + 2) >> 2;
+        v = (k > 0 && k < 4 * n) ? f : v;                       // the two end samples stay unfiltered
     }
     auto ref = [&](int i) { return __builtin_amdgcn_ds_bpermute((base + i) << 2, v); };
     auto uref = [&](int i) {                                     // reference i of this lane's half, uniform per half
@@ -348,40 +356,46 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     int pred;
     if (mode == 0) {
         const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
-        pred = ((n - 1 - x) * lft + (x + 1) * uref(3 * n + 1) + (n - 1 - y) * top + (y + 1) * uref(n - 1) + n) >> (LOG2 + 1);
+        pred = (__mul24(n - 1 - x, lft) + __mul24(x + 1, uref(3 * n + 1)) + __mul24(n - 1 - y, top) +
+                __mul24(y + 1, uref(n - 1)) + n) >> (LOG2 + 1);
     } else if (mode == 1) {
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
         const int dc = (wave_sum<PAIR>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
-        const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
-        pred = dc;
-        if (!PAIR) {                                             // luma n < 32: edge smoothing
-            if (x == 0 && y == 0) pred = (lft + 2 * dc + top + 2) >> 2;
-            else if (y == 0) pred = (top + 3 * dc + 2) >> 2;
-            else if (x == 0) pred = (lft + 3 * dc + 2) >> 2;
+        if (PAIR) {
+            pred = dc;
+        } else {                                                 // luma n < 32: edge smoothing
+            const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
+            // (lft + 2dc + top + 2) >> 2 at (0,0); one-sided (3dc + side + 2) >> 2 on row 0 / column 0
+            const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
+            pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
         }
     } else {
         const int ang = (int)(int8_t)(w1 & 0xffu);
         const int inv = -(int)((w1 >> 8) & 0x1fffu);
         const bool vert = mode >= 18;
         const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
-        const int idx = ((along + 1) * ang) >> 5, fact = ((along + 1) * ang) & 31;
+        const int pa = __mul24(along + 1, ang);
+        const int idx = pa >> 5, fact = pa & 31;
         const int r0 = across + idx + 1;
         auto refk = [&](int r) {                                 // r < 0: projected side reference (invAngle)
-            const int t = r >= 0 ? r : -((r * inv + 128) >> 8);
+            const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
             return vert ? 2 * n + t : 2 * n - t;
         };
         const bool bflt = !PAIR && (mode == 26 || mode == 10);
         const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : refk(r0 + 1);
         const int a = ref(refk(r0)), b = ref(i1);
-        pred = fact ? ((32 - fact) * a + fact * b + 16) >> 5 : a;
-        if (bflt) {
-            const int corner = uref(2 * n);
-            if (vert && x == 0) pred = clip_pel(uref(2 * n + 1) + ((b - corner) >> 1), maxv);
-            if (!vert && y == 0) pred = clip_pel(uref(2 * n - 1) + ((b - corner) >> 1), maxv);
+        pred = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;   // = a when iFact = 0 (b then unused)
+        if (bflt) {                                              // modes 26 / 10, luma: boundary smoothing
+            const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
+            pred = (vert ? x : y) == 0 ? edge : pred;
         }
     }
+    // every lane stores (no exec-mask juggling): lanes without a sample of this job write a
+    // private byte of the (here unused) reference scratch area
     const bool own = hl < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
-    if (own) org[y * ist + x] = (uint8_t)clip_pel(pred + r16, maxv);
+    const uint32_t da = own ? orgA + y * ist + x : (uint32_t)(uintptr_t)&L.ref[0][0] + lane;
+    const int res = ((w0 >> (28 + half)) & 1u) ? r16 : 0;      // coded: the loaded sample, else 0
+    *reinterpret_cast<uint8_t*>(lds_ptr(da)) = (uint8_t)clip_pel(pred + res, maxv);
     wave_sync();
 }
 
@@ -481,8 +495,6 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             const uint32_t tb_begin = uniform(gload(reinterpret_cast<const uint2*>(ctus + addr))).x;
             const int nt = (int)__builtin_amdgcn_readfirstlane(*gptr(jcount + addr));
             const IntraJob* jl = jobs + tb_begin;
-            uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
-            if (lane < nt) { rec0 = ld16(&jl[lane].w[0]); rec1 = ld16(&jl[lane].w[4]); }
             // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr)
             const uint8_t* ltop_l = line_up + x0;
             const uint8_t* ltop_c = line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
@@ -511,35 +523,42 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const uint32_t o = cod ? (h ? w4 : w3) + (uint32_t)(hl < (1 << (2 * lg)) ? hl : 0) : 0u;
                 return base + o;
             };
-            uint32_t w0n = 0, w1n = 0, w2n = 0, w5n = 0;
+            // job records: 64 at a time into two VGPRs per lane, read per job with v_readlane
+            // (scalar loads were measured slower: their lgkmcnt waits serialise with the LDS
+            // traffic of the job)
+            struct JobS { uint32_t w0, w1, w2, w3, w4, w5; };
+            uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
+            auto refill = [&](int base) {
+                if (base + lane < nt) { rec0 = ld16(&jl[base + lane].w[0]); rec1 = ld16(&jl[base + lane].w[4]); }
+                else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
+            };
+            auto sjob = [&](int i) {
+                const int l = i & 63;
+                auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane(v, l); };
+                return JobS{rl(rec0.x), rl(rec0.y), rl(rec0.z), rl(rec0.w), rl(rec1.x), rl(rec1.y)};
+            };
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
             int r16n = 0;
-            auto fetch = [&](int l) {                            // job l of the current record block
-                w0n = __builtin_amdgcn_readlane(rec0.x, l);
-                w1n = __builtin_amdgcn_readlane(rec0.y, l);
-                w2n = __builtin_amdgcn_readlane(rec0.z, l);
-                w5n = __builtin_amdgcn_readlane(rec1.y, l);
-                const uint32_t w3 = __builtin_amdgcn_readlane(rec0.w, l), w4 = __builtin_amdgcn_readlane(rec1.x, l);
-                if (w5n & J5_FAST) {
-                    const int16_t* a = res_fast(w0n, w3, w4);
-                    r16n = *gptr(a);
+            auto issue = [&](const JobS& j) {                    // residual loads of job j
+                if (j.w5 & J5_FAST) {
+                    r16n = *gptr(res_fast(j.w0, j.w3, j.w4));
                 } else {
-                    const uint4* a = res_addr(w0n, w3, w4);
+                    const uint4* a = res_addr(j.w0, j.w3, j.w4);
                     ra = ld16(a); rb = ld16(a + 1);
                 }
             };
-            if (nt) fetch(0);
+            JobS cur{0, 0, 0, 0, 0, 0};
+            if (nt) { refill(0); cur = sjob(0); issue(cur); }
             for (int t = 0; t < nt; ++t) {
-                const uint32_t w0 = w0n, w1 = w1n, w2 = w2n, w5 = w5n;
+                // next job's record and residual are fetched before this job runs; this job
+                // works on copies of its own (measured: issuing after the job is slower)
+                const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w5 = cur.w5;
                 const uint4 ca = ra, cb = rb;
-                const int cr16 = ((w0 >> (28 + ((w0 >> 15) & 3u ? (lane >> 5) : 0))) & 1u) ? r16n : 0;
+                const int c16 = r16n;
                 if (t + 1 < nt) {
-                    const int l = (t + 1) & 63;
-                    if (l == 0) {
-                        if (t + 1 + lane < nt) { rec0 = ld16(&jl[t + 1 + lane].w[0]); rec1 = ld16(&jl[t + 1 + lane].w[4]); }
-                        else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
-                    }
-                    fetch(l);
+                    if (((t + 1) & 63) == 0) refill(t + 1);
+                    cur = sjob(t + 1);
+                    issue(cur);
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
                 // Opaque copies of the lane id and the LDS bases: keeps the compiler from
@@ -556,9 +575,9 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_FAST) {
                     switch (sel) {
-                        case 0: recon_fast<2, false>(LL, tlp, w0, w1, w5, cr16, ln); break;
-                        case 1: recon_fast<3, false>(LL, tlp, w0, w1, w5, cr16, ln); break;
-                        default: recon_fast<2, true>(LL, tcp, w0, w1, w5, cr16, ln); break;
+                        case 0: recon_fast<2, false>(LL, tlp, w0, w1, w5, c16, ln); break;
+                        case 1: recon_fast<3, false>(LL, tlp, w0, w1, w5, c16, ln); break;
+                        default: recon_fast<2, true>(LL, tcp, w0, w1, w5, c16, ln); break;
                     }
                 } else switch (sel) {
                     case 0: recon_job<2, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;

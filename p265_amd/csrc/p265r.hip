@@ -73,8 +73,12 @@ struct p265r_ctx {
     Geo geo{};
     int n_ctus = 0;
     bool timing = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    p265r_timings last{};
+    // per timed run: 4 events (start, after residual, after intra, after loop filter) + the
+    // launch counts; kept for every run since p265r_set_timing(ctx, 1) so runs can be queued
+    // back to back and read once (p265r_timings_total)
+    struct Run { hipEvent_t ev[4]; p265r_timings counts; };
+    std::vector<Run> runs;
+    std::vector<hipEvent_t> spare;
     bool have_timing = false;
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
@@ -257,7 +261,6 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
     if (e == hipSuccess) {
         int8_t ang[35];
         int16_t inv[35];
@@ -278,7 +281,8 @@ void p265r_destroy(p265r_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->pending) { (void)hipStreamSynchronize(ctx->stream); p265r_batch_free(ctx, ctx->pending); }
-    for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
+    for (auto& e : ctx->spare) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -433,7 +437,14 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     hipStream_t s = ctx->stream;
     const Geo& g = ctx->geo;
     p265r_timings tm{};
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (ctx->timing) {
+        for (auto& e : ev) {
+            if (!ctx->spare.empty()) { e = ctx->spare.back(); ctx->spare.pop_back(); }
+            else HIP_TRY(hipEventCreate(&e));
+        }
+        HIP_TRY(hipEventRecord(ev[0], s));
+    }
     // ---- residual phase ----------------------------------------------------------
     const int bdl = g.bd[0], bdc = g.bd[1];
     if (b->n_jobs[RC_DST4]) {
@@ -473,7 +484,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     HIP_TRY(hipGetLastError());
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] residual phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] residual phase done\n"); }
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ev[1], s));
     // ---- intra wavefront ---------------------------------------------------------------
     if (ctx->schedule == 1) {
         HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int), s));
@@ -493,7 +504,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     HIP_TRY(hipGetLastError());
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
     if (b->dbk || b->sao) {
         const long long units = (long long)ctx->n_ctus * b->n_pics;
@@ -511,9 +522,14 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
     }
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[3], s));
-    ctx->last = tm;
-    ctx->have_timing = ctx->timing;
+    if (ctx->timing) {
+        HIP_TRY(hipEventRecord(ev[3], s));
+        p265r_ctx::Run run;
+        for (int i = 0; i < 4; ++i) run.ev[i] = ev[i];
+        run.counts = tm;
+        ctx->runs.push_back(run);
+        ctx->have_timing = true;
+    }
     return P265R_OK;
 }
 
@@ -584,21 +600,50 @@ int p265r_sync(p265r_ctx* ctx) {
 int p265r_set_timing(p265r_ctx* ctx, int enable) {
     if (!ctx) return P265R_EINVAL;
     ctx->timing = enable != 0;
+    if (enable) {                               // start a new accumulation
+        for (auto& r : ctx->runs) for (auto& e : r.ev) ctx->spare.push_back(e);
+        ctx->runs.clear();
+        ctx->have_timing = false;
+    }
     return P265R_OK;
 }
 
+namespace {
+int run_times(const p265r_ctx::Run& r, p265r_timings* t) {
+    HIP_TRY(hipEventSynchronize(r.ev[3]));
+    float a = 0, b = 0, c = 0, tt = 0;
+    HIP_TRY(hipEventElapsedTime(&a, r.ev[0], r.ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, r.ev[1], r.ev[2]));
+    HIP_TRY(hipEventElapsedTime(&c, r.ev[2], r.ev[3]));
+    HIP_TRY(hipEventElapsedTime(&tt, r.ev[0], r.ev[3]));
+    *t = r.counts;
+    t->residual_ms = a; t->intra_ms = b; t->sao_ms = c; t->total_ms = tt;
+    return P265R_OK;
+}
+}  // namespace
+
 int p265r_last_timings(p265r_ctx* ctx, p265r_timings* out) {
     if (!ctx || !out) return P265R_EINVAL;
-    if (!ctx->have_timing) return P265R_ESTATE;
-    HIP_TRY(hipEventSynchronize(ctx->ev[3]));
-    float a = 0, b = 0, c = 0, t = 0;
-    HIP_TRY(hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
-    HIP_TRY(hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]));
-    HIP_TRY(hipEventElapsedTime(&c, ctx->ev[2], ctx->ev[3]));
-    HIP_TRY(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[3]));
-    p265r_timings r = ctx->last;
-    r.residual_ms = a; r.intra_ms = b; r.sao_ms = c; r.total_ms = t;
-    *out = r;
+    if (!ctx->have_timing || ctx->runs.empty()) return P265R_ESTATE;
+    HIP_TRY(hipSetDevice(ctx->device));
+    return run_times(ctx->runs.back(), out);
+}
+
+int p265r_timings_total(p265r_ctx* ctx, p265r_timings* out, int* n_runs) {
+    if (!ctx || !out) return P265R_EINVAL;
+    if (!ctx->have_timing || ctx->runs.empty()) return P265R_ESTATE;
+    HIP_TRY(hipSetDevice(ctx->device));
+    p265r_timings sum{};
+    for (const auto& r : ctx->runs) {
+        p265r_timings t{};
+        int rc = run_times(r, &t);
+        if (rc) return rc;
+        sum.total_ms += t.total_ms; sum.residual_ms += t.residual_ms; sum.intra_ms += t.intra_ms; sum.sao_ms += t.sao_ms;
+        sum.intra_launches += t.intra_launches; sum.residual_launches += t.residual_launches;
+        sum.sao_launches += t.sao_launches;
+    }
+    if (n_runs) *n_runs = (int)ctx->runs.size();
+    *out = sum;
     return P265R_OK;
 }
 

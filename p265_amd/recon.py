@@ -138,6 +138,15 @@ class ReconContext:
     def set_timing(self, on=True):
         _lib.check(self.lib.p265r_set_timing(self.handle, int(bool(on))), "p265r_set_timing")
 
+    def timings_total(self):
+        """Sums of the per-phase times over every run since set_timing(True), and the run count."""
+        t = _lib.Timings()
+        n = ctypes.c_int(0)
+        _lib.check(self.lib.p265r_timings_total(self.handle, ctypes.byref(t), ctypes.byref(n)), "p265r_timings_total")
+        d = {f: getattr(t, f) for f, _ in _lib.Timings._fields_ if f != "reserved"}
+        d["runs"] = n.value
+        return d
+
     def last_timings(self):
         t = _lib.Timings()
         _lib.check(self.lib.p265r_last_timings(self.handle, ctypes.byref(t)), "p265r_last_timings")
