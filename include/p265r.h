@@ -50,6 +50,12 @@ extern "C" {
 #define P265R_TB_BYPASS  0x04u  /* cu_transquant_bypass_flag (cu.py:102-105)                 */
 #define P265R_TB_PCM     0x08u  /* PCM block: coef holds samples at BitDepth; no prediction    */
 
+/* p265r_picture.flags */
+#define P265R_PIC_RECON_INPUT 0x01u /* recon[] holds the reconstruction (input): residual and intra
+                                       phases are skipped, only the in-loop filters run (tile halo
+                                       decoding, p265_amd/tiles.py).  All pictures of a batch must
+                                       agree on this flag. */
+
 /* p265r_ctu.flags */
 #define P265R_CTU_LF_ACROSS_SLICES 0x01u  /* slice_loop_filter_across_slices_enabled_flag of its slice */
 #define P265R_CTU_DEBLOCK          0x02u  /* deblocking on in its slice (!slice_deblocking_filter_disabled_flag,
@@ -115,7 +121,7 @@ typedef struct p265r_picture {
     const p265r_ctu* ctus;    /* PicSizeInCtbsY entries, raster order                          */
     const p265r_tb*  tbs;
     uint32_t         n_tbs;
-    uint32_t         reserved0;
+    uint32_t         flags;   /* P265R_PIC_*                                                   */
     const int16_t*   coef;
     uint64_t         n_coef;
     const uint8_t*   nofilter;/* optional (NULL): per 8x8 luma block, raster, ceil(W/8) wide;
@@ -124,7 +130,8 @@ typedef struct p265r_picture {
     void*            out[3];  /* decoded (post-deblocking, post-SAO) planes Y, Cb, Cr; stride =
                                  plane width; uint8_t samples (8-bit).  NULL = do not download */
     void*            recon[3];/* optional in-loop-filter input (reconstruction before deblocking
-                                 and SAO), same layout; NULL = skip                             */
+                                 and SAO), same layout; NULL = skip.  Written by download, or
+                                 read by upload with P265R_PIC_RECON_INPUT                     */
 } p265r_picture;
 
 /* Per-phase device time of the last run, from HIP events on the context's stream. */

@@ -47,7 +47,7 @@ class Params(ctypes.Structure):
 
 class PictureC(ctypes.Structure):
     _fields_ = [("ctus", ctypes.c_void_p), ("tbs", ctypes.c_void_p), ("n_tbs", ctypes.c_uint32),
-                ("reserved0", ctypes.c_uint32), ("coef", ctypes.c_void_p), ("n_coef", ctypes.c_uint64),
+                ("flags", ctypes.c_uint32), ("coef", ctypes.c_void_p), ("n_coef", ctypes.c_uint64),
                 ("nofilter", ctypes.c_void_p), ("out", ctypes.c_void_p * 3), ("recon", ctypes.c_void_p * 3)]
 
 

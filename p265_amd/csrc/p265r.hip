@@ -101,6 +101,7 @@ struct p265r_batch {
     std::vector<DevPic> h_pics;
     bool sao = false;
     bool dbk = false;          // some CTU of the batch has deblocking on
+    bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
 };
 
 namespace {
@@ -109,6 +110,8 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     const p265r_params& p = ctx->params;
     const Geo& g = ctx->geo;
     if (!pic.ctus || (!pic.tbs && pic.n_tbs) || (!pic.coef && pic.n_coef)) return P265R_EINVAL;
+    if (pic.flags & ~P265R_PIC_RECON_INPUT) return P265R_EINVAL;
+    if ((pic.flags & P265R_PIC_RECON_INPUT) && (!pic.recon[0] || !pic.recon[1] || !pic.recon[2])) return P265R_EINVAL;
     const int ctb = 1 << p.ctb_log2_size;
     for (int rs = 0; rs < ctx->n_ctus; ++rs) {
         const p265r_ctu& c = pic.ctus[rs];
@@ -293,7 +296,9 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     for (int i = 0; i < n_pics; ++i) {
         int rc = validate_picture(ctx, pics[i]);
         if (rc) return rc;
+        if ((pics[i].flags ^ pics[0].flags) & P265R_PIC_RECON_INPUT) return P265R_EINVAL;
     }
+    const bool recon_input = (pics[0].flags & P265R_PIC_RECON_INPUT) != 0;
     const Geo& g = ctx->geo;
     const int nc = ctx->n_ctus;
     // ---- pool sizing per class ---------------------------------------------------
@@ -364,6 +369,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->n_pics = n_pics;
     b->sao = sao;
     b->dbk = dbk;
+    b->recon_input = recon_input;
     unsigned char* dbase = static_cast<unsigned char*>(b->mem);
     b->d_pics = reinterpret_cast<DevPic*>(dbase + o_pics);
     b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
@@ -427,6 +433,13 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     std::memcpy(host.data() + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
     e = hipMemcpy(b->mem, host.data(), o_rec, hipMemcpyHostToDevice);
     if (e != hipSuccess) { int rc = hip_fail(e, "hipMemcpy(upload)"); (void)hipFree(b->mem); delete b; return rc; }
+    if (recon_input) {
+        const int wd[3] = {g.w, g.cw, g.cw}, ht[3] = {g.h, g.ch, g.ch};
+        for (int i = 0; i < n_pics && e == hipSuccess; ++i)
+            for (int c = 0; c < 3 && e == hipSuccess; ++c)
+                e = hipMemcpy2D(b->h_pics[i].rec[c], g.stride[c], pics[i].recon[c], wd[c], wd[c], ht[c], hipMemcpyHostToDevice);
+        if (e != hipSuccess) { int rc = hip_fail(e, "hipMemcpy2D(recon input)"); (void)hipFree(b->mem); delete b; return rc; }
+    }
     *out = b;
     return P265R_OK;
 }
@@ -447,31 +460,32 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     // ---- residual phase ----------------------------------------------------------
     const int bdl = g.bd[0], bdc = g.bd[1];
-    if (b->n_jobs[RC_DST4]) {
+    const bool recon = !b->recon_input;
+    if (recon && b->n_jobs[RC_DST4]) {
         residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl);
         ++tm.residual_launches;
     }
-    if (b->n_jobs[RC_DCT4]) {
+    if (recon && b->n_jobs[RC_DCT4]) {
         residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc);
         ++tm.residual_launches;
     }
-    if (b->n_jobs[RC_DCT8]) {
+    if (recon && b->n_jobs[RC_DCT8]) {
         residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (b->n_jobs[RC_DCT16]) {
+    if (recon && b->n_jobs[RC_DCT16]) {
         residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (b->n_jobs[RC_DCT32]) {
+    if (recon && b->n_jobs[RC_DCT32]) {
         residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (b->n_jobs[RC_TSKIP]) {
+    if (recon && b->n_jobs[RC_TSKIP]) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (ctx->schedule == 1) {
+    if (recon && ctx->schedule == 1) {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
         // of the residuals, timed with the residual phase
         intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
@@ -486,13 +500,13 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] residual phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] residual phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[1], s));
     // ---- intra wavefront ---------------------------------------------------------------
-    if (ctx->schedule == 1) {
+    if (recon && ctx->schedule == 1) {
         HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int), s));
         int rc = launch_rows(ctx, b);
         if (rc) return rc;
         ++tm.intra_launches;
     }
-    const int n_steps = ctx->schedule == 0 ? (g.wc - 1) + 2 * (g.hc - 1) + 1 : 0;
+    const int n_steps = (recon && ctx->schedule == 0) ? (g.wc - 1) + 2 * (g.hc - 1) + 1 : 0;
     for (int step = 0; step < n_steps; ++step) {
         const int d = step - (g.wc - 1);
         const int cy_min = d > 0 ? (d + 1) / 2 : 0;
@@ -543,7 +557,7 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
             if (pics[i].out[c])
                 HIP_TRY(hipMemcpy2DAsync(pics[i].out[c], wd[c], b->h_pics[i].out[c], g.stride[c], wd[c], ht[c],
                                          hipMemcpyDeviceToHost, ctx->stream));
-            if (pics[i].recon[c])
+            if (pics[i].recon[c] && !b->recon_input)
                 HIP_TRY(hipMemcpy2DAsync(pics[i].recon[c], wd[c], b->h_pics[i].rec[c], g.stride[c], wd[c], ht[c],
                                          hipMemcpyDeviceToHost, ctx->stream));
         }

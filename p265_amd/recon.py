@@ -104,6 +104,14 @@ class ReconContext:
                     c.out[k] = outs[i][k].ctypes.data
                 if recons is not None:
                     c.recon[k] = recons[i][k].ctypes.data
+            if p.recon_input is not None:
+                c.flags = R.PIC_RECON_INPUT
+                planes = [np.ascontiguousarray(p.recon_input[k], np.uint8) for k in range(3)]
+                for k, (pl, shp) in enumerate(zip(planes, plane_shapes(self.params))):
+                    if pl.shape != shp:
+                        raise R.RecordError("recon_input plane %d has shape %s, expected %s" % (k, pl.shape, shp))
+                    c.recon[k] = pl.ctypes.data
+                keep += planes
         return arr, keep
 
     def _alloc_planes(self, n):
@@ -155,7 +163,7 @@ class ReconContext:
     # ---- one-shot API (submit / wait) -------------------------------------------------
     def decode(self, pics, with_recon=False):
         outs = self._alloc_planes(len(pics))
-        recs = self._alloc_planes(len(pics)) if with_recon else None
+        recs = self._alloc_planes(len(pics)) if with_recon and pics[0].recon_input is None else None
         arr, keep = self._pictures_c(pics, outs, recs)
         _lib.check(self.lib.p265r_submit(self.handle, arr, len(pics)), "p265r_submit")
         _lib.check(self.lib.p265r_wait(self.handle), "p265r_wait")

@@ -20,6 +20,7 @@ import numpy as np
 ABI_VERSION = 1
 
 TB_CBF, TB_TSKIP, TB_BYPASS, TB_PCM = 0x01, 0x02, 0x04, 0x08
+PIC_RECON_INPUT = 0x01
 CTU_LF_ACROSS_SLICES, CTU_DEBLOCK = 0x01, 0x02
 
 PARAMS_DTYPE = np.dtype([
@@ -95,6 +96,9 @@ class Picture:
     coef: np.ndarray                      # int16
     nofilter: Optional[np.ndarray] = None  # uint8 per 8x8 luma block or None
     meta: dict = field(default_factory=dict)
+    # P265R_PIC_RECON_INPUT: the reconstruction [Y, Cb, Cr] (uint8) is given; only the
+    # in-loop filters run on it (TB records then serve the deblocking map only)
+    recon_input: Optional[list] = None
 
     def as_oracle_dict(self):
         return {"ctus": self.ctus, "tbs": self.tbs, "coef": self.coef, "nofilter": self.nofilter}

@@ -4,9 +4,9 @@ With tiles, intra prediction never crosses a tile edge (6.4.1: a neighbour in an
 tile is unavailable; decoder/image.py:65-71), and when
 loop_filter_across_tiles_enabled_flag is 0 neither does SAO (8.7.3.2).  A tile is then
 exactly a picture of its own size: ``split`` re-bases a picture's records onto one
-tile, ``stitch`` puts decoded tiles back.  (With the flag at 1, the SAO of the
-1-sample tile border needs the neighbour tile's pre-SAO samples: a halo exchange,
-not implemented in this round -- ``split`` refuses it.)
+tile, ``stitch`` puts decoded tiles back.  With the flag at 1, deblocking and SAO of a
+tile's border need the neighbour tiles' samples: ``split(recon_only=True)`` gives the
+reconstruction pass and p265_amd/halo.py the halo exchange + filtering pass.
 """
 import numpy as np
 
@@ -22,10 +22,17 @@ def tile_grid(params, pic):
     return cols, rows
 
 
-def split(params, pic):
-    """[(tile_params, tile_picture, (x0, y0) luma origin)] for every tile, in tile-scan order."""
-    if int(params["loop_filter_across_tiles"]):
-        raise NotImplementedError("tile split with loop_filter_across_tiles_enabled_flag=1 needs a halo exchange")
+def split(params, pic, recon_only=False):
+    """[(tile_params, tile_picture, (x0, y0) luma origin)] for every tile, in tile-scan order.
+
+    With loop_filter_across_tiles_enabled_flag = 1 a tile's in-loop filters need its
+    neighbours' samples: split then only serves the reconstruction pass (``recon_only``:
+    in-loop filter flags cleared) and p265_amd/halo.py does the filtering."""
+    if int(params["loop_filter_across_tiles"]) and not recon_only:
+        raise NotImplementedError("loop_filter_across_tiles_enabled_flag=1: split(recon_only=True) + halo.py")
+    if recon_only:
+        from .halo import recon_only as _ro
+        params, pic = _ro(params, pic)
     ctb_log2 = int(params["ctb_log2_size"])
     ctb = 1 << ctb_log2
     w, h = int(params["pic_width"]), int(params["pic_height"])

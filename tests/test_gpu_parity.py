@@ -234,3 +234,44 @@ def test_sao_only_window_kernel(recon_mod):
         pics = [synth.make_picture(params, 1700 + s, perf=False, tiles=(2, 1), n_slices=3, lf_across_slices=None,
                                    bypass_rate=0.05) for s in range(2)]
         _check_c(recon_mod, params, pics, "sao-only")
+
+
+# ---------------------------------------------------------------------------------
+# C5 with loop_filter_across_tiles_enabled_flag = 1: tile reconstruction + halo + filtering
+# ---------------------------------------------------------------------------------
+
+def _tile_halo_decode(recon_mod, params, pic):
+    """Every tile on its own through the library (reconstruction pass, then the in-loop
+    filters on its extended tile with the neighbours' halos): stitched tile outputs."""
+    from p265_amd import halo, tiles
+    grid = halo.TileGrid.from_picture(params, pic)
+    datas = []
+    for t, (tp, tpic, _) in enumerate(tiles.split(params, pic, recon_only=True)):
+        with recon_mod.ReconContext(tp) as ctx:
+            out = ctx.decode([tpic])[0]                  # no in-loop filters in this pass: out = recon
+        d = halo.TileData(grid, pic, t)
+        d.recon = out
+        datas.append(d)
+    outs = {}
+    for t in range(grid.n_tiles):
+        ep, epic, origin, inner = halo.ext_picture(params, grid, datas[t], [datas[n].halo_for(t) for n in grid.neighbours(t)])
+        with recon_mod.ReconContext(ep) as ctx:
+            outs[t] = halo.crop_inner(ctx.decode([epic])[0], origin, inner)
+    return grid, outs
+
+
+@pytest.mark.parametrize("w,h,ctb_log2,tiles_xy,perf", [(264, 200, 5, (2, 2), False), (200, 136, 4, (3, 2), False),
+                                                        (3840, 2160, 6, (2, 2), True)])
+def test_tile_halo_equals_whole_picture(recon_mod, w, h, ctb_log2, tiles_xy, perf):
+    from oracle import c_oracle
+    params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2, loop_filter_across_tiles=1,
+                           pps_cb_qp_offset=1, pps_cr_qp_offset=-2)
+    pic = synth.make_picture(params, 2024 + w, perf=perf, tiles=tiles_xy, n_slices=1 if perf else 3,
+                             lf_across_slices=None, deblocking="random", bypass_rate=0.03)
+    grid, outs = _tile_halo_decode(recon_mod, params, pic)
+    ref = c_oracle.decode(params, [pic], threads=8)[0][1]
+    for t, planes in outs.items():
+        x0, x1, y0, y1 = grid.luma_rect(grid.rect(t))
+        for c in range(3):
+            s = 0 if c == 0 else 1
+            np.testing.assert_array_equal(planes[c], ref[c][y0 >> s:y1 >> s, x0 >> s:x1 >> s], err_msg="tile %d c%d" % (t, c))
