@@ -32,7 +32,7 @@ namespace p265r {
 //  w2: availability bits 0..31 (unit u: k in [u*us, u*us+us) for u < L, corner u = L,
 //      top units u > L; us = 4 luma / 2 chroma samples, L = 2N/us)
 //  w3, w4: residual element offset of half 0 (luma / Cb) and half 1 (Cr)
-//  w5: fast-path job (intra_rows.h recon_fast): bit 31 set for luma 4x4 / 8x8 and Cb+Cr
+//  w5: fast-path job (intra_rows.h recon_fast*): bit 31 set for luma 4x4 .. 16x16 and Cb+Cr
 //      4x4 pairs, not PCM, whose available reference samples form ONE contiguous run
 //      [fa, la] of the linear order (or none): substitution (8.4.4.2.2) is then
 //      s = Clip3(fa, la, k).  fa bits 0..7, la bits 8..15.
@@ -117,7 +117,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             J.w[4] = off1;
             // fast path: one contiguous run of available units -> sample bounds [fa, la]
             uint32_t w5 = 0;
-            const bool fast_size = (c == 0 && n <= 8) || (cm == 3u && n == 4);
+#ifndef P265R_FAST16
+#define P265R_FAST16 1
+#endif
+            const bool fast_size = (c == 0 && n <= (P265R_FAST16 ? 16 : 8)) || (cm == 3u && n == 4);
             if (fast_size && !(f0 & P265R_TB_PCM)) {
                 const int US = c ? 1 : 2;
                 if (m == 0) {

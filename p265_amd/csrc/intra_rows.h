@@ -399,6 +399,110 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     wave_sync();
 }
 
+// Fast 16x16 luma job (J5_FAST): as recon_fast, 65 reference samples (lane k holds
+// sample k, sample 64 is wave-uniform), 4 predicted samples per lane (a row quarter),
+// residual (4 samples) in rw.x / rw.y, one 4-byte LDS store per lane.
+__device__ __forceinline__ void recon_fast16(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
+                                             uint32_t w5, uint4 rw, int lane) {
+    constexpr int n = 16, LOG2 = 4, ist = 64, maxv = 255;
+    const int ofs = (int)(w0 & 0x1fffu);
+    const int xr = ofs & 63, yr = ofs >> 6;
+    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + ofs;
+    const uint8_t* const lcol = L.yleft + yr;
+    const int mode = (int)((w0 >> 17) & 63u);
+    const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
+    const uint32_t orgA = (uint32_t)(uintptr_t)org, lcolA = (uint32_t)(uintptr_t)lcol;
+    const uint32_t ltA = (uint32_t)(uintptr_t)line_top + xr;
+    const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
+    const int ls = xr == 0 ? 1 : ist;
+    const uint32_t tb = (yr == 0 ? ltA : orgA - ist) - 2 * n - 1;
+    const int th = 2 * n + (yr > 0 ? 1 : 0);
+    auto addr = [&](int sref) { return tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u); };
+    const bool none = (w0 & J_NONE) != 0;
+    const int k = lane;
+    const int raw = (int)*reinterpret_cast<const uint8_t*>(lds_ptr(addr(min(max(k, fa), la))));
+    const int raw64 = (int)*reinterpret_cast<const uint8_t*>(lds_ptr(addr(min(max(4 * n, fa), la))));
+    int v = none ? 128 : raw;
+    const int r64 = none ? 128 : __builtin_amdgcn_readfirstlane(raw64);     // reference sample 64 (end, unfiltered)
+    if ((w0 >> 24) & 3u) {                                    // [1 2 1] (8.4.4.2.3)
+        const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
+        const int vr0 = __builtin_amdgcn_ds_bpermute(min(k + 1, 63) << 2, v);
+        const int vr = k == 63 ? r64 : vr0;
+        const int f = (vl + 2 * v + vr + 2) >> 2;
+        v = k > 0 ? f : v;
+    }
+    auto ref = [&](int i) {                                   // reference i, 0..64
+        const int b = __builtin_amdgcn_ds_bpermute(min(i, 63) << 2, v);
+        return i >= 64 ? r64 : b;
+    };
+    auto uref = [&](int i) { return i >= 64 ? r64 : (int)__builtin_amdgcn_readlane(v, i); };
+    const int x0 = (lane & 3) << 2, y = lane >> 2;           // samples (x0 .. x0 + 3, y)
+    int pred[4];
+    if (mode == 0) {
+        const int lft = ref(2 * n - 1 - y), trs = uref(3 * n + 1), bls = uref(n - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int x = x0 + i;
+            pred[i] = (__mul24(n - 1 - x, lft) + __mul24(x + 1, trs) + __mul24(n - 1 - y, ref(2 * n + 1 + x)) +
+                       __mul24(y + 1, bls) + n) >> (LOG2 + 1);
+        }
+    } else if (mode == 1) {
+        const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
+        const int dc = (wave_sum<false>(in ? v : 0, 0) + n) >> (LOG2 + 1);
+        const int lft = ref(2 * n - 1 - y);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int x = x0 + i;
+            const int top = ref(2 * n + 1 + x);
+            const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
+            pred[i] = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
+        }
+    } else {
+        const int ang = (int)(int8_t)(w1 & 0xffu);
+        const int inv = -(int)((w1 >> 8) & 0x1fffu);
+        auto refk = [&](int r, bool vert) {
+            const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
+            return vert ? 2 * n + t : 2 * n - t;
+        };
+        if (mode >= 18) {                                     // vertical: one projection row per lane
+            const int pa = __mul24(y + 1, ang);
+            const int idx = pa >> 5, fact = pa & 31;
+            int q[5];
+#pragma unroll
+            for (int m = 0; m < 5; ++m) q[m] = ref(refk(x0 + idx + 1 + m, true));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pred[i] = (__mul24(32 - fact, q[i]) + __mul24(fact, q[i + 1]) + 16) >> 5;
+            if (mode == 26) {                                 // x == 0: boundary smoothing
+                const int e = clip_pel(uref(2 * n + 1) + ((ref(2 * n - 1 - y) - uref(2 * n)) >> 1), maxv);
+                pred[0] = x0 == 0 ? e : pred[0];
+            }
+        } else {                                              // horizontal: projection column per sample
+            const int corner = uref(2 * n), left0 = uref(2 * n - 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int x = x0 + i;
+                const int pa = __mul24(x + 1, ang);
+                const int idx = pa >> 5, fact = pa & 31;
+                const int r0 = y + idx + 1;
+                const int a = ref(refk(r0, false));
+                const int b = ref(mode == 10 ? 2 * n + 1 + x : refk(r0 + 1, false));
+                pred[i] = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;
+                if (mode == 10) pred[i] = y == 0 ? clip_pel(left0 + ((b - corner) >> 1), maxv) : pred[i];
+            }
+        }
+    }
+    const bool coded = (w0 >> 28) & 1u;
+    uint32_t out = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t wd = i < 2 ? rw.x : rw.y;
+        const int res = coded ? (int)(int16_t)(wd >> (16 * (i & 1))) : 0;
+        out |= (uint32_t)clip_pel(pred[i] + res, maxv) << (8 * i);
+    }
+    *reinterpret_cast<uint32_t*>(lds_ptr(orgA + y * ist + x0)) = out;
+    wave_sync();
+}
+
 template <int W>
 __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
@@ -540,7 +644,12 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
             int r16n = 0;
             auto issue = [&](const JobS& j) {                    // residual loads of job j
-                if (j.w5 & J5_FAST) {
+                if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) {        // 16x16 luma: 4 samples per lane
+                    const int16_t* base = ((j.w0 >> 26) & 1u) ? pool : resid;
+                    const uint32_t o = ((j.w0 >> 28) & 1u) ? j.w3 + 4u * (uint32_t)lane : 0u;
+                    const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(base + o));
+                    ra = make_uint4(d.x, d.y, 0u, 0u);
+                } else if (j.w5 & J5_FAST) {
                     r16n = *gptr(res_fast(j.w0, j.w3, j.w4));
                 } else {
                     const uint4* a = res_addr(j.w0, j.w3, j.w4);
@@ -577,6 +686,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                     switch (sel) {
                         case 0: recon_fast<2, false>(LL, tlp, w0, w1, w5, c16, ln); break;
                         case 1: recon_fast<3, false>(LL, tlp, w0, w1, w5, c16, ln); break;
+                        case 2: recon_fast16(LL, tlp, w0, w1, w5, ca, ln); break;
                         default: recon_fast<2, true>(LL, tcp, w0, w1, w5, c16, ln); break;
                     }
                 } else switch (sel) {
