@@ -83,7 +83,7 @@ struct p265r_ctx {
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
-    int row_waves = 16;        // waves per workgroup of the row pipeline (4, 8 or 16)
+    int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16); 8 = 2 workgroups per CU
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
 };
