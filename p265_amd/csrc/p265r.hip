@@ -147,8 +147,10 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
 template <int W>
 int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
     const Geo& g = ctx->geo;
-    // picture slots: enough for the W rows in flight to span, plus one of slack
-    int fs = std::min(32, (W + g.hc - 1) / g.hc + 2);
+    // picture slots: the W rows in flight are consecutive in the queue, so they span at
+    // most ceil(W / hc) + 1 pictures; a slot is reused only after its previous picture is
+    // complete (the kernel waits for that, so fewer slots would still be correct)
+    int fs = std::min(32, (W + g.hc - 1) / g.hc + 1);
     auto lds_of = [&](int f) {
         return 256 + (size_t)((f * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
     };
