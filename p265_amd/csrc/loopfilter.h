@@ -160,6 +160,10 @@ struct LfCtu {                  // the fields of a neighbouring CTU record the f
     uint8_t  offs;
 };
 
+#ifndef P265R_LF_DBK_THREADS
+#define P265R_LF_DBK_THREADS 192
+#endif
+
 template <int CTBL> struct LfShape {
     static constexpr int S = 1 << CTBL, SC = S / 2;
     static constexpr int RL = S + 8, RC = SC + 8;          // window rows (halo 4) and used columns
@@ -176,7 +180,13 @@ template <int CTBL> struct LfShape {
     static constexpr int NLE = S / 8 + 1, NCE = SC / 8 + 1;   // edges per direction
     static constexpr int N_DBK = NLE * WL + 2 * NCE * WC;     // 4-line segments per direction
     static constexpr int T0 = N_SAO > N_DBK ? N_SAO : N_DBK;
-    static constexpr int THREADS = (T0 + 63) / 64 * 64;
+    static constexpr int T1 = (T0 + 63) / 64 * 64;
+    // with deblocking, at most three waves per workgroup: smaller workgroups let more CTB windows
+    // be in flight per CU (the kernel is bound by load latency, not by issue).  Measured, 1080p
+    // CTB 64, 512 pictures: 64 / 128 / 192 / 256 threads -> 3.62 / 2.83 / 2.64 / 3.42 ms.  SAO
+    // alone prefers one unit per thread (256: 1.65 ms, 128: 1.73 ms).  Every phase loops over
+    // its tasks, so any multiple of 64 is correct.
+    static constexpr int threads(bool dbk) { return dbk && T1 > P265R_LF_DBK_THREADS ? P265R_LF_DBK_THREADS : T1; }
 };
 
 // grid (CTUs, pictures); DBK: deblock the window first (else the window is the SAO input as is)
@@ -192,7 +202,7 @@ __device__ __forceinline__ int xcd_unit(int b, int n_units) {
 // grid (8 * ceil(CTUs * pictures / 8)); DBK: deblock the window first (else the window is
 // the SAO input as is)
 template <int CTBL, bool DBK>
-__global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(const DevPic* __restrict__ pics, Geo g,
+__global__ __launch_bounds__(LfShape<CTBL>::threads(DBK)) void loopfilter_kernel(const DevPic* __restrict__ pics, Geo g,
                                                                           int sao_on, int n_pics) {
     using SH = LfShape<CTBL>;
     constexpr int S = SH::S, SC = SH::SC, WL = SH::WL, WC = SH::WC, NB = SH::NB;
@@ -216,7 +226,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
     const int rx = rs % g.wc, ry = rs / g.wc;
     const int x0 = rx * S, y0 = ry * S, xc0 = x0 >> 1, yc0 = y0 >> 1;
     const int tid = threadIdx.x;
-    constexpr int T = SH::THREADS;
+    constexpr int T = SH::threads(DBK);
     const p265r_ctu me = ctus[rs];
 
     // ---- CTU neighbourhood, SAO permissions (8.7.3.2), map windows, sample windows ---------------
@@ -389,13 +399,13 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
         }
     }
 
-    // ---- SAO of the CTB from the (deblocked) window; one thread per UL / UC-sample row unit ----
+    // ---- SAO of the CTB from the (deblocked) window; one UL / UC-sample row unit per task ----
     const uint32_t allow = s_allow;
-    if (tid >= SH::N_SAO) return;
+    for (int u = tid; u < SH::N_SAO; u += T) {
     int c, t;
     constexpr int NL = S * (S / SH::UL), NC = SC * (SC / SH::UC);
-    if (tid < NL) { c = 0; t = tid; }
-    else { c = 1 + (tid - NL) / NC; t = (tid - NL) % NC; }
+    if (u < NL) { c = 0; t = u; }
+    else { c = 1 + (u - NL) / NC; t = (u - NL) % NC; }
     const int sub = c ? 1 : 0;
     const int U = c ? SH::UC : SH::UL;                 // samples per unit (16 or 8)
     const int NW = U / 4;
@@ -405,7 +415,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
     const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
     const int xb = c ? xc0 : x0, yb = c ? yc0 : y0;
     const int X = xb + col, Y = yb + row;
-    if (X >= W || Y >= H) return;
+    if (X >= W || Y >= H) continue;
     const uint32_t* win = c ? s_cw(c - 1) : s_l;
     const int wst = c ? PC : PL;
     // window dword (r, d) holds samples (xb - 4 + 4d .. +3, yb - 4 + r)
@@ -526,6 +536,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::THREADS) void loopfilter_kernel(cons
     uint8_t* dst = P->out[c] + (size_t)Y * g.stride[c] + X;
     if (NW == 4) *reinterpret_cast<uint4*>(dst) = make_uint4(res[0], res[1], res[2], res[3]);
     else *reinterpret_cast<uint2*>(dst) = make_uint2(res[0], res[1]);
+    }
 }
 
 }  // namespace p265r

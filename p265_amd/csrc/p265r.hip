@@ -528,12 +528,12 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         const dim3 grid((unsigned)((units + 7) / 8 * 8));
         const int so = b->sao ? 1 : 0, np = b->n_pics;
         switch (g.ctb_log2 * 2 + (b->dbk ? 1 : 0)) {
-            case 12: loopfilter_kernel<6, false><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
-            case 13: loopfilter_kernel<6, true><<<grid, LfShape<6>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
-            case 10: loopfilter_kernel<5, false><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
-            case 11: loopfilter_kernel<5, true><<<grid, LfShape<5>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
-            case 8: loopfilter_kernel<4, false><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
-            default: loopfilter_kernel<4, true><<<grid, LfShape<4>::THREADS, 0, s>>>(b->d_pics, g, so, np); break;
+            case 12: loopfilter_kernel<6, false><<<grid, LfShape<6>::threads(false), 0, s>>>(b->d_pics, g, so, np); break;
+            case 13: loopfilter_kernel<6, true><<<grid, LfShape<6>::threads(true), 0, s>>>(b->d_pics, g, so, np); break;
+            case 10: loopfilter_kernel<5, false><<<grid, LfShape<5>::threads(false), 0, s>>>(b->d_pics, g, so, np); break;
+            case 11: loopfilter_kernel<5, true><<<grid, LfShape<5>::threads(true), 0, s>>>(b->d_pics, g, so, np); break;
+            case 8: loopfilter_kernel<4, false><<<grid, LfShape<4>::threads(false), 0, s>>>(b->d_pics, g, so, np); break;
+            default: loopfilter_kernel<4, true><<<grid, LfShape<4>::threads(true), 0, s>>>(b->d_pics, g, so, np); break;
         }
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
