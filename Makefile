@@ -5,7 +5,15 @@ HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -shared -Wall -Wno-unuse
 SRC := p265_amd/csrc/p265r.hip
 HDR := $(wildcard p265_amd/csrc/*.h) include/p265r.h
 
-all: p265_amd/libp265r.so oracle
+CXX ?= g++
+FESRC := $(wildcard p265_amd/csrc/fe/*.cpp)
+FEHDR := $(wildcard p265_amd/csrc/fe/*.h) include/p265fe.h include/p265r.h
+
+all: p265_amd/libp265r.so p265_amd/libp265fe.so oracle
+
+# native syntax front-end (host C++, no GPU code)
+p265_amd/libp265fe.so: $(FESRC) $(FEHDR)
+	$(CXX) -O3 -std=c++17 -fPIC -shared -pthread -Wall -Wextra -Wno-unused-parameter -o $@ $(FESRC)
 
 p265_amd/libp265r.so: $(SRC) $(HDR)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
@@ -14,7 +22,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f p265_amd/libp265r.so
+	rm -f p265_amd/libp265r.so p265_amd/libp265fe.so
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,0 +1,145 @@
+"""ctypes binding of libp265fe.so: the native HEVC syntax front-end (include/p265fe.h).
+
+Replaces the reference's Python parse loop (dec.py:18-64 -> nalu.py -> slice.py ->
+ctu.py / cu.py / tu.py / sao.py with the CABAC engine of cabac.py) for all-intra
+streams.  ``decode_stream(data)`` parses a whole Annex-B byte stream on host threads
+and returns, per picture in decode order, the back-end records that the reference's
+per-CU hook would have produced (``records.Picture``) plus the picture's params,
+POC, output rank, conformance window and decoded-picture hash.
+
+There is no fallback: a missing library raises ``LibraryNotFound``; a malformed or
+unsupported stream raises ``BitstreamError`` / ``UnsupportedStream``.
+"""
+import ctypes
+import os
+import threading
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from . import records as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("P265FE_LIB", os.path.join(HERE, "libp265fe.so"))
+
+OK, EINVAL, ENOMEM, EUNSUPPORTED, EBITSTREAM = 0, -1, -2, -4, -8
+HASH_NONE, HASH_MD5, HASH_CRC, HASH_CHECKSUM = -1, 0, 1, 2
+
+
+class BitstreamError(ValueError):
+    pass
+
+
+class UnsupportedStream(BitstreamError):
+    pass
+
+
+class PictureInfoC(ctypes.Structure):
+    _fields_ = [("params", _lib.Params), ("ctus", ctypes.c_void_p), ("tbs", ctypes.c_void_p),
+                ("n_tbs", ctypes.c_uint32), ("n_ctus", ctypes.c_uint32), ("coef", ctypes.c_void_p),
+                ("n_coef", ctypes.c_uint64), ("nofilter", ctypes.c_void_p), ("poc", ctypes.c_int32),
+                ("output_rank", ctypes.c_int32), ("crop_left", ctypes.c_uint16), ("crop_right", ctypes.c_uint16),
+                ("crop_top", ctypes.c_uint16), ("crop_bottom", ctypes.c_uint16), ("nal_unit_type", ctypes.c_uint8),
+                ("hash_type", ctypes.c_int8), ("n_slices", ctypes.c_uint16), ("n_cus", ctypes.c_uint32),
+                ("hash", (ctypes.c_uint8 * 16) * 3)]
+
+
+_vp = ctypes.c_void_p
+SIGNATURES = {
+    "p265fe_create": (ctypes.c_int, [ctypes.POINTER(_vp)]),
+    "p265fe_destroy": (None, [_vp]),
+    "p265fe_decode": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]),
+    "p265fe_picture": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PictureInfoC)]),
+    "p265fe_last_error": (ctypes.c_char_p, [_vp]),
+    "p265fe_abi_version": (ctypes.c_uint32, []),
+}
+
+_lock = threading.Lock()
+_handle = None
+
+
+def load():
+    global _handle
+    with _lock:
+        if _handle is None:
+            if not os.path.exists(LIB_PATH):
+                raise _lib.LibraryNotFound("%s not built (run `make` or __graft_entry__.build())" % LIB_PATH)
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype, fn.argtypes = res, args
+            if lib.p265fe_abi_version() != 1:
+                raise _lib.LibraryNotFound("libp265fe.so ABI version mismatch")
+            _handle = lib
+        return _handle
+
+
+@dataclass
+class DecodedPicture:
+    """One picture of the stream: back-end records + stream-level metadata."""
+    params: np.ndarray
+    picture: R.Picture
+    poc: int
+    output_rank: int            # -1: not output (pic_output_flag 0 / RASL after a CRA start)
+    crop: tuple                 # conformance window (left, right, top, bottom) in luma samples
+    nal_unit_type: int
+    n_slices: int
+    n_cus: int
+    hash_type: int
+    hash: Optional[list]        # per component bytes of the decoded picture hash SEI
+
+
+def _params_np(pc):
+    kw = {name: getattr(pc, name) for name, _ in _lib.Params._fields_ if name not in ("version", "reserved")}
+    return R.make_params(**kw)
+
+
+def _copy(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype)
+    buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=n).copy()
+
+
+def decode_stream(data: bytes, threads: int = 0, validate: bool = True):
+    """Parse an Annex-B HEVC byte stream; returns [DecodedPicture] in decode order."""
+    lib = load()
+    h = ctypes.c_void_p()
+    if lib.p265fe_create(ctypes.byref(h)) != OK:
+        raise MemoryError("p265fe_create failed")
+    try:
+        n = lib.p265fe_decode(h, bytes(data), len(data), int(threads))
+        if n < 0:
+            msg = lib.p265fe_last_error(h).decode(errors="replace")
+            cls = UnsupportedStream if n == EUNSUPPORTED else BitstreamError
+            raise cls("p265fe_decode: %s (%d)" % (msg, n))
+        out = []
+        info = PictureInfoC()
+        for i in range(n):
+            rc = lib.p265fe_picture(h, i, ctypes.byref(info))
+            if rc != OK:
+                raise BitstreamError("p265fe_picture(%d) failed (%d)" % (i, rc))
+            params = _params_np(info.params)
+            ctus = _copy(info.ctus, info.n_ctus, R.CTU_DTYPE)
+            tbs = _copy(info.tbs, info.n_tbs, R.TB_DTYPE)
+            coef = _copy(info.coef, int(info.n_coef), np.int16)
+            nof = None
+            if info.nofilter:
+                w, hh = int(params["pic_width"]), int(params["pic_height"])
+                nof = _copy(info.nofilter, ((w + 7) // 8) * ((hh + 7) // 8), np.uint8)
+            pic = R.Picture(ctus=ctus, tbs=tbs, coef=coef, nofilter=nof,
+                            meta={"poc": int(info.poc), "decode_index": i})
+            if validate:
+                R.validate(params, pic)
+            hl = {HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}.get(int(info.hash_type))
+            hv = [bytes(info.hash[c][:hl]) for c in range(3)] if hl else None
+            out.append(DecodedPicture(params=params, picture=pic, poc=int(info.poc),
+                                      output_rank=int(info.output_rank),
+                                      crop=(info.crop_left, info.crop_right, info.crop_top, info.crop_bottom),
+                                      nal_unit_type=int(info.nal_unit_type), n_slices=int(info.n_slices),
+                                      n_cus=int(info.n_cus), hash_type=int(info.hash_type), hash=hv))
+        return out
+    finally:
+        lib.p265fe_destroy(h)

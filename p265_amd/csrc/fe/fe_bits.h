@@ -1,0 +1,236 @@
+// Bit-level readers of the native front-end: NAL unit extraction, RBSP bit reader
+// (u(n), ue(v), se(v)) and the CABAC arithmetic decoding engine (H.265 9.3.4.3).
+//
+// Replaces the reference's BitStreamBuffer (decoder/bsb.py:6-176: search_start_code,
+// read_bits, u, ue, se) and the engine half of decoder/cabac.py (Cabac.decode_decision,
+// decode_bypass, decode_terminate, renormalization_process: cabac.py:219-293).  The
+// reference reads the byte stream bit by bit through Python calls; here a NAL unit is
+// first turned into its RBSP (emulation_prevention_three_byte removed) and the engine
+// keeps 7 look-ahead bits in a 16-bit window, refilled a byte at a time.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace p265fe {
+
+struct BitstreamError : std::runtime_error {
+    explicit BitstreamError(const std::string& s) : std::runtime_error(s) {}
+};
+struct Unsupported : std::runtime_error {
+    explicit Unsupported(const std::string& s) : std::runtime_error(s) {}
+};
+
+[[noreturn]] inline void bs_fail(const char* what) { throw BitstreamError(what); }
+
+// One NAL unit of an Annex-B byte stream: header fields + RBSP bytes.
+struct Nal {
+    int type = 0, layer_id = 0, temporal_id = 0;
+    std::vector<uint8_t> rbsp;   // payload after the 2-byte header, emulation prevention removed
+};
+
+// Split an Annex-B byte stream at start codes (0x000001 / 0x00000001), dropping
+// trailing_zero_8bits, and convert each NAL unit payload to RBSP (7.3.1.1, 7.4.2).
+inline std::vector<Nal> split_nals(const uint8_t* d, size_t n) {
+    std::vector<Nal> out;
+    size_t i = 0;
+    auto find_sc = [&](size_t from) -> size_t {
+        for (size_t k = from; k + 2 < n; ++k)
+            if (d[k] == 0 && d[k + 1] == 0 && d[k + 2] == 1) return k;
+        return n;
+    };
+    i = find_sc(0);
+    while (i < n) {
+        size_t start = i + 3;
+        size_t next = find_sc(start);
+        size_t end = next;
+        while (end > start && d[end - 1] == 0) --end;   // zero_byte of the next start code / trailing zeros
+        if (end - start >= 2) {
+            Nal nal;
+            uint16_t h = (uint16_t)((d[start] << 8) | d[start + 1]);
+            if (h & 0x8000) bs_fail("forbidden_zero_bit set");
+            nal.type = (h >> 9) & 63;
+            nal.layer_id = (h >> 3) & 63;
+            nal.temporal_id = (int)(h & 7) - 1;
+            if (nal.temporal_id < 0) bs_fail("nuh_temporal_id_plus1 == 0");
+            nal.rbsp.reserve(end - start);
+            int zeros = 0;
+            for (size_t k = start + 2; k < end; ++k) {
+                uint8_t b = d[k];
+                if (zeros >= 2 && b == 3) { zeros = 0; continue; }  // emulation_prevention_three_byte
+                zeros = (b == 0) ? zeros + 1 : 0;
+                nal.rbsp.push_back(b);
+            }
+            out.push_back(std::move(nal));
+        }
+        i = next;
+    }
+    return out;
+}
+
+// MSB-first bit reader over an RBSP (u(n), ue(v), se(v): 7.2, 9.2).
+class BitReader {
+public:
+    BitReader(const uint8_t* p, size_t n, size_t bitpos = 0) : p_(p), n_(n), pos_(bitpos) {}
+    uint32_t u(int bits) {
+        uint32_t v = 0;
+        for (int k = 0; k < bits; ++k) v = (v << 1) | bit();
+        return v;
+    }
+    uint32_t bit() {
+        if (pos_ >= n_ * 8) bs_fail("read past end of RBSP");
+        uint32_t b = (p_[pos_ >> 3] >> (7 - (pos_ & 7))) & 1;
+        ++pos_;
+        return b;
+    }
+    uint32_t ue() {
+        int lz = 0;
+        while (!bit()) {
+            if (++lz > 31) bs_fail("ue(v) too long");
+        }
+        if (lz == 0) return 0;
+        uint64_t v = ((uint64_t)1 << lz) - 1 + u(lz);
+        if (v > 0xFFFFFFFEull) bs_fail("ue(v) overflow");
+        return (uint32_t)v;
+    }
+    int32_t se() {
+        uint32_t k = ue();
+        return (k & 1) ? (int32_t)((k + 1) >> 1) : -(int32_t)(k >> 1);
+    }
+    bool flag() { return bit() != 0; }
+    void skip(size_t bits) { pos_ += bits; if (pos_ > n_ * 8) bs_fail("skip past end of RBSP"); }
+    bool byte_aligned() const { return (pos_ & 7) == 0; }
+    size_t pos() const { return pos_; }
+    size_t size_bits() const { return n_ * 8; }
+    // byte_alignment(): alignment_bit_equal_to_one + zero bits (7.3.2.11)
+    void byte_alignment() {
+        if (bit() != 1) bs_fail("alignment_bit_equal_to_one != 1");
+        while (!byte_aligned())
+            if (bit() != 0) bs_fail("alignment_bit_equal_to_zero != 0");
+    }
+    // more_rbsp_data() (7.2): anything before the rbsp_stop_one_bit?
+    bool more_rbsp_data() const {
+        size_t last = n_;
+        while (last > 0 && p_[last - 1] == 0) --last;
+        if (last == 0) return false;
+        uint8_t b = p_[last - 1];
+        int tz = 0;
+        while (!((b >> tz) & 1)) ++tz;
+        size_t stop = (last - 1) * 8 + (7 - tz);   // bit index of rbsp_stop_one_bit
+        return pos_ < stop;
+    }
+
+private:
+    const uint8_t* p_;
+    size_t n_;
+    size_t pos_;
+};
+
+// ---------------------------------------------------------------------------------
+// CABAC arithmetic decoding engine (9.3.4.3).  Context state byte = (pStateIdx << 1) | valMps.
+// ---------------------------------------------------------------------------------
+extern const uint8_t kLpsTable[64][4];      // rangeTabLps (Table 9-46; cabac.py:66-132)
+extern const uint8_t kNextStateMps[64];     // transIdxMps (Table 9-47; cabac.py:134-143)
+extern const uint8_t kNextStateLps[64];     // transIdxLps (cabac.py:145-154)
+
+class Cabac {
+public:
+    // Start (or restart) the engine at byte `byte_pos` of the RBSP (9.3.2.5: ivlCurrRange = 510,
+    // ivlOffset = read_bits(9)).
+    void start(const uint8_t* rbsp, size_t n, size_t byte_pos) {
+        base_ = rbsp;
+        end_ = rbsp + n;
+        cur_ = rbsp + (byte_pos < n ? byte_pos : n);
+        range_ = 510;
+        value_ = (uint32_t)next_byte() << 8;
+        value_ |= next_byte();
+        bits_needed_ = -8;
+    }
+    inline int decision(uint8_t& ctx) {
+        uint32_t state = ctx >> 1, mps = ctx & 1;
+        uint32_t lps = kLpsTable[state][(range_ >> 6) & 3];
+        range_ -= lps;
+        uint32_t scaled = range_ << 7;
+        int bin;
+        if (value_ < scaled) {
+            bin = (int)mps;
+            ctx = (uint8_t)((kNextStateMps[state] << 1) | mps);
+            if (scaled < (256u << 7)) {
+                range_ = scaled >> 6;
+                value_ <<= 1;
+                if (++bits_needed_ == 0) refill();
+            }
+        } else {
+            bin = (int)(1 - mps);
+            value_ -= scaled;
+            int nb = renorm_bits(lps);
+            value_ <<= nb;
+            range_ = lps << nb;
+            if (state == 0) mps = 1 - mps;
+            ctx = (uint8_t)((kNextStateLps[state] << 1) | mps);
+            bits_needed_ += nb;
+            if (bits_needed_ >= 0) {
+                value_ |= (uint32_t)next_byte() << bits_needed_;
+                bits_needed_ -= 8;
+            }
+        }
+        return bin;
+    }
+    inline int bypass() {
+        value_ <<= 1;
+        if (++bits_needed_ >= 0) refill();
+        uint32_t scaled = range_ << 7;
+        if (value_ >= scaled) { value_ -= scaled; return 1; }
+        return 0;
+    }
+    inline uint32_t bypass_bits(int n) {
+        uint32_t v = 0;
+        for (int i = 0; i < n; ++i) v = (v << 1) | (uint32_t)bypass();
+        return v;
+    }
+    inline int terminate() {
+        range_ -= 2;
+        uint32_t scaled = range_ << 7;
+        if (value_ >= scaled) return 1;     // no renormalization (9.3.4.3.5)
+        if (scaled < (256u << 7)) {
+            range_ = scaled >> 6;
+            value_ <<= 1;
+            if (++bits_needed_ == 0) refill();
+        }
+        return 0;
+    }
+    // Bit position (in the RBSP) of the spec decoder, which has read 9 bits at start and one
+    // per renormalization shift.  After a terminate bin equal to 1 the last bit read is the
+    // final '1' written by the encoder flush (rbsp_stop_one_bit / alignment_bit_equal_to_one /
+    // the bit before pcm_alignment_zero_bit); the next byte-aligned position follows it.
+    size_t bit_pos() const {
+        return (size_t)((cur_ - base_) * 8 + bits_needed_ + 1);
+    }
+    size_t aligned_byte_after_terminate() const { return (bit_pos() + 7) >> 3; }
+    bool overrun() const { return bit_pos() > (size_t)(end_ - base_) * 8; }
+
+private:
+    static inline int renorm_bits(uint32_t r) {   // shifts to bring r (>= 2) back to >= 256
+        return __builtin_clz(r) - 23;
+    }
+    inline uint32_t next_byte() {
+        if (cur_ < end_) return *cur_++;
+        ++overrun_;
+        ++cur_;
+        return 0;
+    }
+    inline void refill() {
+        bits_needed_ = -8;
+        value_ |= next_byte();
+    }
+    const uint8_t* base_ = nullptr;
+    const uint8_t* end_ = nullptr;
+    const uint8_t* cur_ = nullptr;
+    uint32_t range_ = 510, value_ = 0;
+    int bits_needed_ = -8;
+    int overrun_ = 0;
+};
+
+}  // namespace p265fe

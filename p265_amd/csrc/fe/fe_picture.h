@@ -1,0 +1,34 @@
+// Slice segment data decoding of one picture into back-end records (see fe_picture.cpp).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "../../../include/p265r.h"
+#include "fe_ps.h"
+
+namespace p265fe {
+
+struct PictureRecords {
+    std::vector<p265r_ctu> ctus;      // raster order
+    std::vector<p265r_tb> tbs;        // grouped by CTU (raster), decode order inside a CTU
+    std::vector<int16_t> coef;        // decode order
+    std::vector<uint8_t> nofilter;    // empty = none
+    uint32_t n_cus = 0;
+};
+
+struct SliceRef {
+    const SliceHeader* hdr;
+    const uint8_t* rbsp;
+    size_t size;
+};
+
+// Decode every slice segment of one picture (in decode order) into records.
+// Throws BitstreamError / Unsupported.
+void decode_picture(const Active& act, const std::vector<SliceRef>& slices, PictureRecords& out);
+
+// Context-variable initialization values (Tables 9-5..9-37, initType 0 = I slices), exposed
+// for the tests' parity with decoder/cabac.py:13-63.
+int context_init_values(const uint8_t** vals);
+
+}  // namespace p265fe
