@@ -1,0 +1,110 @@
+"""Encode -> parse round trips for the syntax sanity.bin does not exercise (CPU only).
+
+tests/streamgen.py writes streams from random syntax decisions and builds the records
+the reference's decode_leaf hook would produce for them (frontend.PictureBuilder).
+The native front-end (libp265fe.so) must parse each stream back into exactly those
+records.  The reference cannot parse any of these features (pps.py:61-93 tiles,
+slice.py:177 deblocking override, slice.py:181-189 entry points, slice.py:295
+end_of_subset_one_bit, nalu.py:130 SEI), so parity there rests on this round trip
+plus the spec restatement; the shared syntax is pinned by sanity.bin (test_bitstream.py).
+"""
+import numpy as np
+import pytest
+
+import streamgen
+from p265_amd import bitstream
+
+CASES = {
+    "defaults": dict(),
+    "plain": dict(sign_hiding=False, tskip=False, sao=False, strong=False),
+    "tiles_uniform": dict(tiles=(2, 2)),
+    "tiles_explicit": dict(tiles=([3, 5], [2, 4])),
+    "wpp": dict(wpp=True),
+    "tiles_wpp": dict(tiles=(2, 2), wpp=True),
+    "slices": dict(slices=[(0, False), (13, False), (30, True)]),
+    "dependent_slices_wpp": dict(slices=[(0, False), (5, True), (17, True), (40, False)], wpp=True),
+    "tiles_slices": dict(tiles=(3, 2), slices=[(0, False), (16, False), (20, True)]),
+    "qp_delta_ctb": dict(qp_delta_depth=0),
+    "qp_delta_d1": dict(qp_delta_depth=1),
+    "qp_delta_d2_ctb32": dict(qp_delta_depth=2, ctb_log2=5, width=192, height=128),
+    "pcm_lf_off": dict(pcm=(3, 4, True)),
+    "pcm_bypass": dict(pcm=(3, 3, False), bypass=True),
+    "bypass": dict(bypass=True),
+    "deblocking_override": dict(deblocking="override", slices=[(0, False), (20, False), (33, False)]),
+    "deblocking_off": dict(deblocking="off"),
+    "chroma_qp_offsets": dict(slice_chroma_offsets=(3, -5), cb_qp_offset=-4, cr_qp_offset=6, qp_delta_depth=1),
+    "conformance_window": dict(conf_window=(1, 3, 2, 5), width=136, height=104),
+    "ctb64_ragged": dict(width=200, height=72, ctb_log2=6, max_tb_log2=5, max_th_depth=2),
+    "ctb32_mincb16": dict(ctb_log2=5, min_cb_log2=4, max_tb_log2=5, max_th_depth=3),
+    "poc_idr_period": dict(frames=4, idr_period=3, log2_max_poc_lsb=4),
+    "lf_flags_off": dict(lf_across_tiles=0, tiles=(2, 1), lf_across_slices=0),
+}
+
+
+def roundtrip(seed, threads=2, **cfg):
+    g = streamgen.StreamGen(seed, **cfg)
+    data, pics = g.stream()
+    dec = bitstream.decode_stream(data, threads=threads)
+    assert len(dec) == len(pics)
+    for d, (prm, p, poc) in zip(dec, pics):
+        assert d.params.tobytes() == prm.tobytes()
+        assert d.poc == poc
+        assert np.array_equal(d.picture.ctus, p.ctus)
+        assert np.array_equal(d.picture.tbs, p.tbs)
+        assert np.array_equal(d.picture.coef, p.coef)
+        if p.nofilter is None:
+            assert d.picture.nofilter is None
+        else:
+            assert np.array_equal(d.picture.nofilter, p.nofilter)
+    return g, dec
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("seed", [0, 1])
+def test_roundtrip(name, seed):
+    roundtrip(1000 + 17 * seed + len(name), **CASES[name])
+
+
+def test_tile_and_slice_records():
+    g, dec = roundtrip(7, tiles=(2, 2), slices=[(0, False), (24, False), (30, True)])
+    ctus = dec[0].picture.ctus
+    assert sorted(set(int(t) for t in ctus["tile_id"])) == [0, 1, 2, 3]
+    # slice 2 starts at tile-scan address 24 -> SliceAddrRs of its CTBs; the dependent segment keeps it
+    addrs = sorted(set(int(a) for a in ctus["slice_addr"]))
+    assert addrs == [0, g.ts_to_rs[24]]
+
+
+def test_conformance_window_and_counts():
+    g, dec = roundtrip(9, conf_window=(1, 3, 2, 5), width=136, height=104)
+    assert dec[0].crop == (2, 6, 4, 10)          # SubWidthC / SubHeightC = 2 for 4:2:0
+    assert dec[0].n_slices == 1 and dec[0].n_cus > 0
+
+
+@pytest.mark.parametrize("kind", ["md5", "crc", "checksum"])
+def test_decoded_picture_hash_sei_is_reported(kind):
+    g = streamgen.StreamGen(11, hash_sei=kind)
+    data, pics = g.stream()
+    dec = bitstream.decode_stream(data)
+    want_type, want = g.last_hash
+    assert dec[0].hash_type == want_type
+    assert dec[0].hash == want
+
+
+def test_output_order_follows_poc_within_each_sequence():
+    g, dec = roundtrip(5, frames=5, idr_period=2)
+    assert [d.poc for d in dec] == [0, 1, 0, 1, 0]
+    assert [d.output_rank for d in dec] == [0, 1, 2, 3, 4]
+    assert [d.nal_unit_type for d in dec] == [19, 1, 19, 1, 19]
+
+
+def test_unsupported_and_missing_parameter_sets():
+    g = streamgen.StreamGen(3)
+    data, _ = g.stream()
+    # drop the SPS: the PPS/slices refer to a missing SPS
+    nals = data.split(b"\x00\x00\x00\x01")[1:]
+    no_sps = b"".join(b"\x00\x00\x00\x01" + n for n in nals if (n[0] >> 1) & 63 != 33)
+    with pytest.raises(bitstream.BitstreamError):
+        bitstream.decode_stream(no_sps)
+    # truncated slice data
+    with pytest.raises(bitstream.BitstreamError):
+        bitstream.decode_stream(data[:len(data) - 40])
