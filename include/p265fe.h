@@ -89,6 +89,11 @@ int  p265fe_decode(p265fe_decoder* dec, const uint8_t* data, size_t size, int n_
 /* Picture i (decode order) of the last p265fe_decode. */
 int  p265fe_picture(p265fe_decoder* dec, int i, p265fe_picture_info* out);
 
+/* Decoded picture hash (D.3.19) of one 8-bit sample plane (width x height, row stride in
+ * bytes): P265FE_HASH_MD5 -> 16 bytes, _CRC -> 2 bytes big-endian, _CHECKSUM -> 4 bytes
+ * big-endian, as carried by the decoded_picture_hash SEI. */
+int  p265fe_plane_hash(const uint8_t* plane, int width, int height, int stride, int hash_type, uint8_t out[16]);
+
 /* Text of the last error of this decoder ("" if none). */
 const char* p265fe_last_error(p265fe_decoder* dec);
 uint32_t    p265fe_abi_version(void);

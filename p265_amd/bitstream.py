@@ -54,6 +54,8 @@ SIGNATURES = {
     "p265fe_picture": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PictureInfoC)]),
     "p265fe_last_error": (ctypes.c_char_p, [_vp]),
     "p265fe_abi_version": (ctypes.c_uint32, []),
+    "p265fe_plane_hash": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_char_p]),
 }
 
 _lock = threading.Lock()
@@ -101,6 +103,17 @@ def _copy(ptr, n, dtype):
         return np.zeros(0, dtype)
     buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
     return np.frombuffer(buf, dtype=dtype, count=n).copy()
+
+
+def plane_hash(plane, hash_type):
+    """decoded_picture_hash value (D.3.19) of one uint8 plane, as the SEI carries it."""
+    lib = load()
+    p = np.ascontiguousarray(plane, np.uint8)
+    out = ctypes.create_string_buffer(16)
+    rc = lib.p265fe_plane_hash(p.ctypes.data, p.shape[1], p.shape[0], p.strides[0], int(hash_type), out)
+    if rc != OK:
+        raise ValueError("p265fe_plane_hash failed (%d)" % rc)
+    return out.raw[:{HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}[int(hash_type)]]
 
 
 def decode_stream(data: bytes, threads: int = 0, validate: bool = True):

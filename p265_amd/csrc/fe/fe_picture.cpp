@@ -310,11 +310,11 @@ private:
             if (type == 1) {
                 for (int i = 0; i < 4; ++i) {
                     int sgn = (absv[i] != 0) ? cabac_.bypass() : 0;
-                    c.sao_offset[ci][i] = (int8_t)((sgn ? -absv[i] : absv[i]) << shift);
+                    c.sao_offset[ci][i] = (int8_t)((sgn ? -absv[i] : absv[i]) * (1 << shift));
                 }
                 c.sao_class[ci] = (uint8_t)cabac_.bypass_bits(5);   // sao_band_position
             } else {
-                for (int i = 0; i < 4; ++i) c.sao_offset[ci][i] = (int8_t)((i >= 2 ? -absv[i] : absv[i]) << shift);
+                for (int i = 0; i < 4; ++i) c.sao_offset[ci][i] = (int8_t)((i >= 2 ? -absv[i] : absv[i]) * (1 << shift));
                 if (ci == 0) c.sao_class[0] = (uint8_t)cabac_.bypass_bits(2);
                 else if (ci == 1) c.sao_class[1] = (uint8_t)cabac_.bypass_bits(2);
                 else c.sao_class[2] = c.sao_class[1];

@@ -422,8 +422,12 @@ class StreamGen:
         return nal(34, bw.bytes())
 
     # ----------------------------------------------------------------- stream
-    def stream(self):
-        """-> (bytes, [(params, records.Picture, poc)] in decode order)."""
+    def stream(self, planes_fn=None):
+        """-> (bytes, [(params, records.Picture, poc)] in decode order).
+
+        With ``hash_sei`` set, each picture is followed by a decoded-picture-hash SEI: of
+        ``planes_fn(params, picture)`` (the decoded Y/Cb/Cr planes, e.g. from the oracle)
+        when given, else random bytes (syntax test only)."""
         c = self.cfg
         out = [self.vps(), self.sps(), self.pps()]
         pics = []
@@ -436,7 +440,12 @@ class StreamGen:
             nal_type = 19 if idr else 1
             nals, pic = self.picture(nal_type, poc % max_lsb)
             out += nals
-            if c["hash_sei"]:
+            if c["hash_sei"] and planes_fn is not None:
+                kind = {"md5": 0, "crc": 1, "checksum": 2}[c["hash_sei"]]
+                hv = picture_hash(planes_fn(self.params, pic), c["hash_sei"])
+                self.last_hash = (kind, hv)
+                out.append(sei_nal(bytes([kind]) + b"".join(hv)))
+            elif c["hash_sei"]:
                 out.append(self.hash_sei_placeholder())
             pics.append((self.params, pic, poc))
             poc += 1
