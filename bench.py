@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--unique", type=int, default=4, help="distinct synthetic pictures per rank (replicated)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the bitstream -> planes end-to-end leg")
     ap.add_argument("--deblocking", action="store_true",
                     help="deblocking on in every slice (real-stream config; SURVEY §8(d) defines the bench without it)")
     return ap.parse_args()
@@ -131,6 +132,37 @@ def cpu_baseline(params, uniq, budget_s):
     return {"value": round(ctus / dt, 1), "unit": "CTU/s", "cores": threads, "kind": "port",
             "sample": "oracle/recon_oracle.c (scalar C restatement, OpenMP over pictures): %d synthetic 1080p "
                       "pictures = %d CTUs in %.1f s" % (n, ctus, dt)}
+
+
+def end_to_end(device, reps=16, threads=16):
+    """Bitstream bytes -> decoded planes in host memory, from a real (synthetic) 1080p stream.
+
+    tests/golden/synth_1080p_4pic.bin (4 IDR pictures with MD5 picture-hash SEI, made by
+    tests/golden/gen_streams.py) is repeated ``reps`` times.  Times the native front-end alone
+    (host threads) and the whole decoder (front-end + record upload + GPU + plane download,
+    i.e. PCIe-inclusive); every decoded picture is checked against its MD5 SEI.  Not ``value``.
+    """
+    from p265_amd import bitstream, decoder
+    path = os.path.join(ROOT, "tests", "golden", "synth_1080p_4pic.bin")
+    if not os.path.exists(path):
+        return {"error": "missing %s" % path}
+    one = open(path, "rb").read()
+    data = one * reps
+    bitstream.decode_stream(one, threads=threads)                  # warm
+    t0 = time.perf_counter()
+    pics = bitstream.decode_stream(data, threads=threads)
+    fe_s = time.perf_counter() - t0
+    n_ctu = sum(len(p.picture.ctus) for p in pics)
+    decoder.decode_bytes(one, device=device)                       # warm (contexts, kernels)
+    t0 = time.perf_counter()
+    frames = decoder.decode_bytes(data, device=device, batch=64, threads=threads)
+    e2e_s = time.perf_counter() - t0
+    return {"stream": "tests/golden/synth_1080p_4pic.bin x%d" % reps, "pictures": len(pics), "ctus": n_ctu,
+            "bytes_per_ctu": round(len(one) * reps / n_ctu, 1), "threads": threads,
+            "frontend_ctu_s": round(n_ctu / fe_s, 1), "frontend_mb_s": round(len(data) / fe_s / 1e6, 2),
+            "e2e_ctu_s": round(n_ctu / e2e_s, 1),
+            "hash_checked": sum(1 for f in frames if f.hash_ok), "hash_failed": sum(1 for f in frames if f.hash_ok is False),
+            "note": "native front-end (libp265fe.so) on host threads + PCIe-inclusive GPU decode; not `value`"}
 
 
 def main():
@@ -211,6 +243,8 @@ def main():
         out["cpu_baseline_c"] = cpu_baseline(params, uniq, a.cpu_baseline_seconds)
     batch.free()
     ctx.close()
+    if rank == 0 and world == 1 and not a.no_e2e:
+        out["end_to_end"] = end_to_end(local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -129,7 +129,8 @@ private:
 };
 
 // ---------------------------------------------------------------------------------
-// CABAC arithmetic decoding engine (9.3.4.3).  Context state byte = (pStateIdx << 1) | valMps.
+// CABAC arithmetic decoding engine (9.3.4.3).  Context state = (pStateIdx << 1) | valMps, kept in a
+// uint16_t (not a char type) so that state writes cannot alias the engine's registers.
 // ---------------------------------------------------------------------------------
 extern const uint8_t kLpsTable[64][4];      // rangeTabLps (Table 9-46; cabac.py:66-132)
 extern const uint8_t kNextStateMps[64];     // transIdxMps (Table 9-47; cabac.py:134-143)
@@ -148,7 +149,7 @@ public:
         value_ |= next_byte();
         bits_needed_ = -8;
     }
-    inline int decision(uint8_t& ctx) {
+    inline int decision(uint16_t& ctx) {
         uint32_t state = ctx >> 1, mps = ctx & 1;
         uint32_t lps = kLpsTable[state][(range_ >> 6) & 3];
         range_ -= lps;
@@ -156,7 +157,7 @@ public:
         int bin;
         if (value_ < scaled) {
             bin = (int)mps;
-            ctx = (uint8_t)((kNextStateMps[state] << 1) | mps);
+            ctx = (uint16_t)((kNextStateMps[state] << 1) | mps);
             if (scaled < (256u << 7)) {
                 range_ = scaled >> 6;
                 value_ <<= 1;
@@ -169,7 +170,7 @@ public:
             value_ <<= nb;
             range_ = lps << nb;
             if (state == 0) mps = 1 - mps;
-            ctx = (uint8_t)((kNextStateLps[state] << 1) | mps);
+            ctx = (uint16_t)((kNextStateLps[state] << 1) | mps);
             bits_needed_ += nb;
             if (bits_needed_ >= 0) {
                 value_ |= (uint32_t)next_byte() << bits_needed_;

@@ -134,6 +134,8 @@ public:
         qp_map_.assign((size_t)min_cb_w_ * min_cb_h_, 0);
         ipm_.assign((size_t)w4_ * h4_, 1);
         ctu_tbs_.assign(a.size_ctb, {});
+        // every sample is covered by at most one coded TB (or PCM block) per component
+        out_.coef.reserve((size_t)sps_.width * sps_.height * 3 / 2);
         out_.ctus.assign(a.size_ctb, p265r_ctu{});
         for (auto& c : out_.ctus) c.flags = P265R_CTU_LF_ACROSS_SLICES;
         qp_bd_y_ = 6 * (sps_.bit_depth_y - 8);
@@ -172,11 +174,11 @@ public:
                 } else if (wpp_row_start) {
                     int trx = cx + 1, try_ = cy - 1;
                     bool avail = trx < W_ && try_ >= 0 && ctb_avail(try_ * W_ + trx);
-                    if (avail && wpp_valid_) std::memcpy(ctx_, wpp_ctx_, C_NUM);
+                    if (avail && wpp_valid_) std::memcpy(ctx_, wpp_ctx_, sizeof(ctx_));
                     else init_contexts();
                 } else if (h.dependent && rs == h.segment_address) {
                     if (!ds_valid_) bs_fail("dependent slice segment without stored contexts");
-                    std::memcpy(ctx_, ds_ctx_, C_NUM);
+                    std::memcpy(ctx_, ds_ctx_, sizeof(ctx_));
                 } else {
                     init_contexts();
                 }
@@ -186,7 +188,7 @@ public:
             first = false;
             decode_ctu(rs, ts);
             if (pps_.entropy_coding_sync && cx == tile_col0 + 1) {   // storage after the 2nd CTB of a tile row
-                std::memcpy(wpp_ctx_, ctx_, C_NUM);
+                std::memcpy(wpp_ctx_, ctx_, sizeof(ctx_));
                 wpp_valid_ = true;
             }
             int end_of_slice_segment = cabac_.terminate();
@@ -206,7 +208,7 @@ public:
             }
         }
         if (pps_.dependent_slice_segments) {
-            std::memcpy(ds_ctx_, ctx_, C_NUM);
+            std::memcpy(ds_ctx_, ctx_, sizeof(ctx_));
             ds_valid_ = true;
         }
     }
@@ -237,7 +239,7 @@ private:
             int pre = clip3(1, 126, ((m * qp) >> 4) + n);
             int mps = pre <= 63 ? 0 : 1;
             int st = mps ? pre - 64 : 63 - pre;
-            ctx_[i] = (uint8_t)((st << 1) | mps);
+            ctx_[i] = (uint16_t)((st << 1) | mps);
         }
     }
     // CTB of a neighbouring location is available: decoded, same slice, same tile (6.4.1)
@@ -653,7 +655,17 @@ private:
         const bool sdh = pps_.sign_data_hiding && !cu_bypass_;
         int greater1_state = 1;   // "c1" carried across sub-blocks (9.3.4.2.6)
         bool first_sb_done = false;
+        // the engine lives in registers for the whole TB (copied back at the end)
+        Cabac e = cabac_;
+        uint16_t* const cx = ctx_;
+        // sig_coeff_flag context per position of a sub-block (9.3.4.2.5), as absolute indices
         static const uint8_t ctx_idx_map[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+        static const uint8_t pattern[4][16] = {
+            {2, 1, 1, 0, 1, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0},     // prevCsbf 0: by xP + yP ([yP][xP] order)
+            {2, 2, 2, 2, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0},     // 1: by yP
+            {2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0},     // 2: by xP
+            {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2}};
+        const int sig_base = C_SIG + (c ? 27 : 0);
         for (int i = last_sb; i >= 0; --i) {
             int xs = sb_scan[i] & 15, ys = sb_scan[i] >> 4;
             int infer_dc = 0;
@@ -661,7 +673,7 @@ private:
                 int right = (xs + 1 < sbw) ? csbf[xs + 1][ys] : 0;
                 int below = (ys + 1 < sbw) ? csbf[xs][ys + 1] : 0;
                 int inc = std::min(right + below, 1) + (c ? 2 : 0);
-                csbf[xs][ys] = (uint8_t)dec(C_CSBF + inc);
+                csbf[xs][ys] = (uint8_t)e.decision(cx[C_CSBF + inc]);
                 infer_dc = 1;
             } else {
                 csbf[xs][ys] = 1;
@@ -674,33 +686,22 @@ private:
                 sig_pos[nsig++] = last_pos;
             }
             if (csbf[xs][ys]) {
-                int prev_csbf = 0;
-                if (log2 > 2) {
-                    if (xs + 1 < sbw) prev_csbf |= csbf[xs + 1][ys];
-                    if (ys + 1 < sbw) prev_csbf |= csbf[xs][ys + 1] << 1;
+                uint8_t sctx[16];
+                if (log2 == 2) {
+                    for (int k = 0; k < 16; ++k) sctx[k] = (uint8_t)(sig_base + ctx_idx_map[k]);
+                } else {
+                    int prev = 0;
+                    if (xs + 1 < sbw) prev |= csbf[xs + 1][ys];
+                    if (ys + 1 < sbw) prev |= csbf[xs][ys + 1] << 1;
+                    int add = c == 0 ? ((xs || ys) ? 3 : 0) + ((log2 == 3) ? (scan == 0 ? 9 : 15) : 21)
+                                     : ((log2 == 3) ? 9 : 12);
+                    for (int k = 0; k < 16; ++k) sctx[k] = (uint8_t)(sig_base + add + pattern[prev][k]);
+                    if (xs == 0 && ys == 0) sctx[0] = (uint8_t)sig_base;   // DC of the TB: sigCtx 0
                 }
                 for (int nn = start; nn >= 0; --nn) {
-                    int xp = c_scan[nn] & 15, yp = c_scan[nn] >> 4;
+                    int pos = c_scan[nn];
                     if (nn > 0 || !infer_dc) {
-                        int sig_ctx;
-                        if (log2 == 2) {
-                            sig_ctx = ctx_idx_map[(yp << 2) + xp];
-                        } else if (xs == 0 && ys == 0 && xp == 0 && yp == 0) {
-                            sig_ctx = 0;
-                        } else {
-                            if (prev_csbf == 0) sig_ctx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
-                            else if (prev_csbf == 1) sig_ctx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
-                            else if (prev_csbf == 2) sig_ctx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
-                            else sig_ctx = 2;
-                            if (c == 0) {
-                                if (xs || ys) sig_ctx += 3;
-                                sig_ctx += (log2 == 3) ? (scan == 0 ? 9 : 15) : 21;
-                            } else {
-                                sig_ctx += (log2 == 3) ? 9 : 12;
-                            }
-                        }
-                        int inc = c ? 27 + sig_ctx : sig_ctx;
-                        if (dec(C_SIG + inc)) {
+                        if (e.decision(cx[sctx[((pos >> 4) << 2) + (pos & 15)]])) {
                             sig_pos[nsig++] = nn;
                             infer_dc = 0;
                         }
@@ -718,9 +719,9 @@ private:
             int g1[16] = {}, g2[16] = {};
             int first_g1_idx = -1;
             int ng1 = std::min(nsig, 8);
+            const int g1_base = C_GT1 + ctx_set * 4 + (c ? 16 : 0);
             for (int k = 0; k < ng1; ++k) {
-                int inc = ctx_set * 4 + greater1_state + (c ? 16 : 0);
-                g1[k] = dec(C_GT1 + inc);
+                g1[k] = e.decision(cx[g1_base + greater1_state]);
                 if (g1[k]) {
                     greater1_state = 0;
                     if (first_g1_idx < 0) first_g1_idx = k;
@@ -728,46 +729,45 @@ private:
                     ++greater1_state;
                 }
             }
-            if (first_g1_idx >= 0) g2[first_g1_idx] = dec(C_GT2 + ctx_set + (c ? 4 : 0));
+            if (first_g1_idx >= 0) g2[first_g1_idx] = e.decision(cx[C_GT2 + ctx_set + (c ? 4 : 0)]);
             bool hidden = sdh && (sig_pos[0] - sig_pos[nsig - 1] > 3);
             // coeff_sign_flag (bypass), last one skipped when hidden
-            uint32_t signs = 0;
             int nsign = hidden ? nsig - 1 : nsig;
-            for (int k = 0; k < nsign; ++k) signs |= (uint32_t)cabac_.bypass() << k;
+            uint32_t signs = nsign ? e.bypass_bits(nsign) << (32 - nsign) : 0;   // first sign in the MSB
             // coeff_abs_level_remaining + levels
-            int rice = 0, sum_abs = 0, num_sig = 0;
+            int rice = 0, sum_abs = 0;
             for (int k = 0; k < nsig; ++k) {
                 int base = 1 + g1[k] + g2[k];
                 int level = base;
-                int thr = (num_sig < 8) ? ((k == first_g1_idx) ? 3 : 2) : 1;
+                int thr = (k < 8) ? ((k == first_g1_idx) ? 3 : 2) : 1;
                 if (base == thr) {
                     int prefix = 0;
-                    while (cabac_.bypass()) {
+                    while (e.bypass()) {
                         if (++prefix > 32) bs_fail("coeff_abs_level_remaining prefix too long");
                     }
                     int rem;
                     if (prefix <= 3) {
-                        rem = (prefix << rice) + (int)cabac_.bypass_bits(rice);
+                        rem = (prefix << rice) + (int)e.bypass_bits(rice);
                     } else {
                         int nb = prefix - 3 + rice;
                         if (nb > 28) bs_fail("coeff_abs_level_remaining too large");
-                        rem = (((1 << (prefix - 3)) + 2) << rice) + (int)cabac_.bypass_bits(nb);
+                        rem = (((1 << (prefix - 3)) + 2) << rice) + (int)e.bypass_bits(nb);
                     }
                     level = base + rem;
                     if (level > 3 * (1 << rice)) rice = std::min(rice + 1, 4);
                 }
-                ++num_sig;
                 int v = level;
-                if (k < nsign) { if ((signs >> k) & 1) v = -v; }
+                if (k < nsign && ((signs << k) & 0x80000000u)) v = -v;
                 if (hidden) {
                     sum_abs += level;
                     if (k == nsig - 1 && (sum_abs & 1)) v = -v;
                 }
-                int nn = sig_pos[k];
-                int x = (xs << 2) + (c_scan[nn] & 15), y = (ys << 2) + (c_scan[nn] >> 4);
+                int pos = c_scan[sig_pos[k]];
+                int x = (xs << 2) + (pos & 15), y = (ys << 2) + (pos >> 4);
                 blk[y * n + x] = (int16_t)clip3(-32768, 32767, v);
             }
         }
+        cabac_ = e;
         return off;
     }
 
@@ -788,7 +788,7 @@ private:
     const uint8_t* rbsp_ = nullptr;
     size_t rbsp_size_ = 0;
     Cabac cabac_;
-    uint8_t ctx_[C_NUM], wpp_ctx_[C_NUM], ds_ctx_[C_NUM];
+    uint16_t ctx_[C_NUM], wpp_ctx_[C_NUM], ds_ctx_[C_NUM];
     bool wpp_valid_ = false, ds_valid_ = false;
     int slice_addr_ = -1, slice_qp_ = 26, cur_tile_ = 0, cur_ctu_ = 0;
     // quantization group state (8.6.1)

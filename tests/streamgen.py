@@ -719,7 +719,8 @@ class StreamGen:
                 inc += 1
             if self._avail(x0, y0 - 1) and self.depth[(y0 - 1) >> mcb, x0 >> mcb] > depth:
                 inc += 1
-            split = int(r.random() < c["split_prob"])
+            sp = c["split_prob"]
+            split = int(r.random() < (sp[log2] if isinstance(sp, dict) else sp))
             enc.decision(self._ctx("split_cu", inc), split)
         else:
             split = int(log2 > mcb)
@@ -838,7 +839,8 @@ class StreamGen:
         c, r, enc, cu = self.cfg, self.rng, self.enc, self.cu
         maxd = c["max_th_depth"] + cu["nxn"]
         if log2 <= c["max_tb_log2"] and log2 > c["min_tb_log2"] and depth < maxd and not (cu["nxn"] and depth == 0):
-            split = int(r.random() < c["tf_split_prob"])
+            sp = c["tf_split_prob"]
+            split = int(r.random() < (sp[log2] if isinstance(sp, dict) else sp))
             enc.decision(self._ctx("split_tf", 5 - log2), split)
         else:
             split = int(log2 > c["max_tb_log2"] or (cu["nxn"] and depth == 0))
