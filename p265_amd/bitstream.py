@@ -98,11 +98,26 @@ def _params_np(pc):
     return R.make_params(**kw)
 
 
-def _copy(ptr, n, dtype):
+class _Owner:
+    """Keeps one p265fe_decoder (and so the record buffers it owns) alive while any array
+    viewing those buffers is alive; destroys it when the last view goes away."""
+
+    def __init__(self, lib, handle):
+        self.lib, self.handle = lib, handle
+
+    def __del__(self):
+        if self.handle:
+            self.lib.p265fe_destroy(self.handle)
+            self.handle = None
+
+
+def _view(ptr, n, dtype, owner):
+    """Zero-copy numpy view of a decoder-owned buffer (no first-touch copy of the records)."""
     if n == 0:
         return np.zeros(0, dtype)
     buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
-    return np.frombuffer(buf, dtype=dtype, count=n).copy()
+    buf._p265fe_owner = owner
+    return np.frombuffer(buf, dtype=dtype, count=n)
 
 
 def plane_hash(plane, hash_type):
@@ -116,43 +131,48 @@ def plane_hash(plane, hash_type):
     return out.raw[:{HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}[int(hash_type)]]
 
 
-def decode_stream(data: bytes, threads: int = 0, validate: bool = True):
-    """Parse an Annex-B HEVC byte stream; returns [DecodedPicture] in decode order."""
+def decode_stream(data: bytes, threads: int = 0, validate: bool = False):
+    """Parse an Annex-B HEVC byte stream; returns [DecodedPicture] in decode order.
+
+    The record arrays are read-only views of the decoder's buffers (kept alive by the
+    arrays).  ``validate`` re-runs the host-side record checks (the back-end's upload
+    validates every record again in C++ before any kernel sees it)."""
     lib = load()
     h = ctypes.c_void_p()
     if lib.p265fe_create(ctypes.byref(h)) != OK:
         raise MemoryError("p265fe_create failed")
-    try:
-        n = lib.p265fe_decode(h, bytes(data), len(data), int(threads))
-        if n < 0:
-            msg = lib.p265fe_last_error(h).decode(errors="replace")
-            cls = UnsupportedStream if n == EUNSUPPORTED else BitstreamError
-            raise cls("p265fe_decode: %s (%d)" % (msg, n))
-        out = []
-        info = PictureInfoC()
-        for i in range(n):
-            rc = lib.p265fe_picture(h, i, ctypes.byref(info))
-            if rc != OK:
-                raise BitstreamError("p265fe_picture(%d) failed (%d)" % (i, rc))
-            params = _params_np(info.params)
-            ctus = _copy(info.ctus, info.n_ctus, R.CTU_DTYPE)
-            tbs = _copy(info.tbs, info.n_tbs, R.TB_DTYPE)
-            coef = _copy(info.coef, int(info.n_coef), np.int16)
-            nof = None
-            if info.nofilter:
-                w, hh = int(params["pic_width"]), int(params["pic_height"])
-                nof = _copy(info.nofilter, ((w + 7) // 8) * ((hh + 7) // 8), np.uint8)
-            pic = R.Picture(ctus=ctus, tbs=tbs, coef=coef, nofilter=nof,
-                            meta={"poc": int(info.poc), "decode_index": i})
-            if validate:
-                R.validate(params, pic)
-            hl = {HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}.get(int(info.hash_type))
-            hv = [bytes(info.hash[c][:hl]) for c in range(3)] if hl else None
-            out.append(DecodedPicture(params=params, picture=pic, poc=int(info.poc),
-                                      output_rank=int(info.output_rank),
-                                      crop=(info.crop_left, info.crop_right, info.crop_top, info.crop_bottom),
-                                      nal_unit_type=int(info.nal_unit_type), n_slices=int(info.n_slices),
-                                      n_cus=int(info.n_cus), hash_type=int(info.hash_type), hash=hv))
-        return out
-    finally:
-        lib.p265fe_destroy(h)
+    owner = _Owner(lib, h)
+    n = lib.p265fe_decode(h, bytes(data), len(data), int(threads))
+    if n < 0:
+        msg = lib.p265fe_last_error(h).decode(errors="replace")
+        cls = UnsupportedStream if n == EUNSUPPORTED else BitstreamError
+        raise cls("p265fe_decode: %s (%d)" % (msg, n))
+    out = []
+    info = PictureInfoC()
+    for i in range(n):
+        rc = lib.p265fe_picture(h, i, ctypes.byref(info))
+        if rc != OK:
+            raise BitstreamError("p265fe_picture(%d) failed (%d)" % (i, rc))
+        params = _params_np(info.params)
+        ctus = _view(info.ctus, info.n_ctus, R.CTU_DTYPE, owner)
+        tbs = _view(info.tbs, info.n_tbs, R.TB_DTYPE, owner)
+        coef = _view(info.coef, int(info.n_coef), np.int16, owner)
+        nof = None
+        if info.nofilter:
+            w, hh = int(params["pic_width"]), int(params["pic_height"])
+            nof = _view(info.nofilter, ((w + 7) // 8) * ((hh + 7) // 8), np.uint8, owner)
+        for arr in (ctus, tbs, coef, nof):
+            if arr is not None:
+                arr.flags.writeable = False
+        pic = R.Picture(ctus=ctus, tbs=tbs, coef=coef, nofilter=nof,
+                        meta={"poc": int(info.poc), "decode_index": i})
+        if validate:
+            R.validate(params, pic)
+        hl = {HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}.get(int(info.hash_type))
+        hv = [bytes(info.hash[c][:hl]) for c in range(3)] if hl else None
+        out.append(DecodedPicture(params=params, picture=pic, poc=int(info.poc),
+                                  output_rank=int(info.output_rank),
+                                  crop=(info.crop_left, info.crop_right, info.crop_top, info.crop_bottom),
+                                  nal_unit_type=int(info.nal_unit_type), n_slices=int(info.n_slices),
+                                  n_cus=int(info.n_cus), hash_type=int(info.hash_type), hash=hv))
+    return out

@@ -84,7 +84,7 @@ class ReconContext:
         keep = []
         arr = (_lib.PictureC * len(pics))()
         for i, p in enumerate(pics):
-            R.validate(self.params, p)
+            R.check_shapes(self.params, p)      # record contents: validated by p265r_batch_upload
             ctus = np.ascontiguousarray(p.ctus, R.CTU_DTYPE)
             tbs = np.ascontiguousarray(p.tbs, R.TB_DTYPE)
             coef = np.ascontiguousarray(p.coef, np.int16)

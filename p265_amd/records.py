@@ -113,6 +113,19 @@ class RecordError(ValueError):
     pass
 
 
+def check_shapes(params, pic: Picture):
+    """The checks the C ABI cannot do itself (array dtypes and lengths behind the raw
+    pointers); everything inside the records is validated again by p265r_batch_upload."""
+    wc, hc = ctb_grid(params)
+    if pic.ctus.dtype != CTU_DTYPE or pic.tbs.dtype != TB_DTYPE or pic.coef.dtype != np.int16:
+        raise RecordError("record dtypes do not match the ABI")
+    if len(pic.ctus) != wc * hc:
+        raise RecordError("expected %d CTUs, got %d" % (wc * hc, len(pic.ctus)))
+    w, h = int(params["pic_width"]), int(params["pic_height"])
+    if pic.nofilter is not None and len(pic.nofilter) != ((w + 7) // 8) * ((h + 7) // 8):
+        raise RecordError("nofilter map has the wrong size")
+
+
 def validate(params, pic: Picture):
     """Host-side checks mirroring the C++ ones (p265_amd/csrc/p265r.hip: validate_picture).
 
@@ -140,8 +153,11 @@ def validate(params, pic: Picture):
     nl = (1 << lg) << sub
     if ((xl >= w) | (yl >= h)).any():
         raise RecordError("TB outside picture")
-    owner = np.repeat(np.arange(len(pic.ctus)), pic.ctus["tb_count"].astype(np.int64))
-    idx = np.concatenate([np.arange(b, e) for b, e in zip(begin, end)]) if len(tbs) else np.zeros(0, np.int64)
+    counts = pic.ctus["tb_count"].astype(np.int64)
+    owner = np.repeat(np.arange(len(pic.ctus)), counts)
+    # idx[k] = TB index of the k-th (CTU, TB) pair: tb_begin of its CTU + rank inside the CTU
+    first = np.cumsum(counts) - counts
+    idx = np.repeat(begin, counts) + (np.arange(int(counts.sum())) - np.repeat(first, counts))
     if len(idx):
         cx, cy = (owner % wc) << ctb_log2, (owner // wc) << ctb_log2
         ctb = 1 << ctb_log2
