@@ -9,12 +9,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/p265r.h"
@@ -86,6 +89,12 @@ struct p265r_ctx {
     int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16); 8 = 2 workgroups per CU
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
+    // reused across batches: pinned host staging (grow-only) and one freed device allocation
+    unsigned char* stage = nullptr;
+    size_t stage_bytes = 0;
+    bool stage_pinned = false;
+    void* cache_mem = nullptr;
+    size_t cache_bytes = 0;
 };
 
 struct p265r_batch {
@@ -105,6 +114,25 @@ struct p265r_batch {
 };
 
 namespace {
+
+// Run fn(i) for i in [0, n) on up to 16 host threads (picture-level packing work).
+template <class F>
+void parallel_for(int n, F fn) {
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = std::min(std::min(hw, 16), n);
+    if (nt <= 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&]() {
+            for (int i; (i = next.fetch_add(1)) < n;) fn(i);
+        });
+    for (auto& t : th) t.join();
+}
 
 int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     const p265r_params& p = ctx->params;
@@ -289,6 +317,8 @@ void p265r_destroy(p265r_ctx* ctx) {
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
     for (auto& e : ctx->spare) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
+    if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
     delete ctx;
 }
 
@@ -303,30 +333,32 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const bool recon_input = (pics[0].flags & P265R_PIC_RECON_INPUT) != 0;
     const Geo& g = ctx->geo;
     const int nc = ctx->n_ctus;
-    // ---- pool sizing per class ---------------------------------------------------
-    size_t pool_sz[N_POOLS] = {};
-    size_t n_tbs_total = 0;
-    for (int i = 0; i < n_pics; ++i) {
-        n_tbs_total += pics[i].n_tbs;
+    // ---- pool sizing per class (per picture, so pictures can be packed in parallel) ----
+    std::vector<std::array<size_t, N_POOLS>> cnt_pool(n_pics);
+    std::vector<std::array<int, RC_NUM>> cnt_job(n_pics);
+    parallel_for(n_pics, [&](int i) {
+        cnt_pool[i].fill(0);
+        cnt_job[i].fill(0);
         for (uint32_t t = 0; t < pics[i].n_tbs; ++t) {
             const p265r_tb& tb = pics[i].tbs[t];
             if (!(tb.flags & (P265R_TB_CBF | P265R_TB_PCM))) continue;
-            pool_sz[tb_class(tb)] += (size_t)1 << (2 * tb.log2_size);
+            const int cls = tb_class(tb);
+            cnt_pool[i][cls] += (size_t)1 << (2 * tb.log2_size);
+            if (cls < RC_NUM) ++cnt_job[i][cls];
         }
+    });
+    size_t pool_sz[N_POOLS] = {};
+    size_t n_tbs_total = 0;
+    int n_jobs[RC_NUM] = {};
+    for (int i = 0; i < n_pics; ++i) {
+        n_tbs_total += pics[i].n_tbs;
+        for (int c = 0; c < N_POOLS; ++c) pool_sz[c] += cnt_pool[i][c];
+        for (int c = 0; c < RC_NUM; ++c) n_jobs[c] += cnt_job[i][c];
     }
     size_t pool_base[N_POOLS];
     size_t pool_total = 0;
     for (int c = 0; c < N_POOLS; ++c) { pool_base[c] = pool_total; pool_total += pool_sz[c]; }
     if (pool_total >= (1ull << 32)) return P265R_ERANGE;
-    int n_jobs[RC_NUM] = {};
-    for (int c = 0; c < RC_NUM; ++c) n_jobs[c] = (int)(pool_sz[c] >> (c == RC_DCT8 ? 6 : c == RC_DCT16 ? 8 : c == RC_DCT32 ? 10 : 4));
-    // transform-skip jobs may have any size: count them exactly
-    n_jobs[RC_TSKIP] = 0;
-    for (int i = 0; i < n_pics; ++i)
-        for (uint32_t t = 0; t < pics[i].n_tbs; ++t) {
-            const p265r_tb& tb = pics[i].tbs[t];
-            if ((tb.flags & P265R_TB_CBF) && tb_class(tb) == RC_TSKIP) ++n_jobs[RC_TSKIP];
-        }
     // ---- device layout -----------------------------------------------------------
     const bool sao = ctx->params.sample_adaptive_offset != 0;
     bool dbk = false;
@@ -359,15 +391,49 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t o_out = off; if (lf) off += pic_plane_bytes * n_pics;
     const size_t total = align_up(off, 256);
 
-    // ---- host staging ------------------------------------------------------------
-    std::vector<unsigned char> host;
-    try { host.resize(o_rec); } catch (...) { return P265R_ENOMEM; }
+    // ---- host staging: [0, o_res) | jobs [o_jobs[0], o_ijobs) | no-filter maps, compact ---------
+    const size_t jobs_bytes = o_ijobs - o_jobs[0];
+    const size_t s_jobs = o_res, s_nf = o_res + jobs_bytes;
+    const size_t stage_need = s_nf + nf_bytes * n_nf;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stage_bytes < stage_need) {
+        if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
+        ctx->stage = nullptr;
+        ctx->stage_bytes = 0;
+        const size_t want = stage_need + stage_need / 4;
+        void* ptr = nullptr;
+        if (hipHostMalloc(&ptr, want, hipHostMallocDefault) == hipSuccess) {
+            ctx->stage_pinned = true;
+        } else {
+            (void)hipGetLastError();
+            ptr = std::malloc(want);
+            ctx->stage_pinned = false;
+            if (!ptr) return P265R_ENOMEM;
+        }
+        ctx->stage = static_cast<unsigned char*>(ptr);
+        ctx->stage_bytes = want;
+    }
+    unsigned char* host = ctx->stage;
     p265r_batch* b = new (std::nothrow) p265r_batch();
     if (!b) return P265R_ENOMEM;
-    (void)hipSetDevice(ctx->device);
-    hipError_t e = hipMalloc(&b->mem, total);
-    if (e != hipSuccess) { delete b; return e == hipErrorOutOfMemory ? P265R_ENOMEM : hip_fail(e, "hipMalloc"); }
-    b->bytes = total;
+    hipError_t e = hipSuccess;
+    if (ctx->cache_mem && ctx->cache_bytes >= total) {      // reuse the last freed allocation
+        b->mem = ctx->cache_mem;
+        b->bytes = ctx->cache_bytes;
+        ctx->cache_mem = nullptr;
+        ctx->cache_bytes = 0;
+    } else {
+        e = hipMalloc(&b->mem, total);
+        if (e != hipSuccess && ctx->cache_mem) {             // make room: drop the cached one
+            (void)hipGetLastError();
+            (void)hipFree(ctx->cache_mem);
+            ctx->cache_mem = nullptr;
+            ctx->cache_bytes = 0;
+            e = hipMalloc(&b->mem, total);
+        }
+        if (e != hipSuccess) { delete b; return e == hipErrorOutOfMemory ? P265R_ENOMEM : hip_fail(e, "hipMalloc"); }
+        b->bytes = total;
+    }
     b->n_pics = n_pics;
     b->sao = sao;
     b->dbk = dbk;
@@ -380,19 +446,37 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     for (int c = 0; c < RC_NUM; ++c) { b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]); b->n_jobs[c] = n_jobs[c]; }
     b->h_pics.resize(n_pics);
 
-    p265r_ctu* h_ctus = reinterpret_cast<p265r_ctu*>(host.data() + o_ctus);
-    p265r_tb* h_tbs = reinterpret_cast<p265r_tb*>(host.data() + o_tbs);
-    int16_t* h_pool = reinterpret_cast<int16_t*>(host.data() + o_pool);
+    p265r_ctu* h_ctus = reinterpret_cast<p265r_ctu*>(host + o_ctus);
+    p265r_tb* h_tbs = reinterpret_cast<p265r_tb*>(host + o_tbs);
+    int16_t* h_pool = reinterpret_cast<int16_t*>(host + o_pool);
     ResJob* h_jobs[RC_NUM];
-    for (int c = 0; c < RC_NUM; ++c) h_jobs[c] = reinterpret_cast<ResJob*>(host.data() + o_jobs[c]);
-    size_t pool_fill[N_POOLS];
-    std::copy(pool_base, pool_base + N_POOLS, pool_fill);
-    int job_fill[RC_NUM] = {};
-    size_t tb_fill = 0, nf_fill = 0;
-    for (int i = 0; i < n_pics; ++i) {
+    for (int c = 0; c < RC_NUM; ++c) h_jobs[c] = reinterpret_cast<ResJob*>(host + s_jobs + (o_jobs[c] - o_jobs[0]));
+    // per-picture start offsets in every pool / job list / TB array / no-filter slot
+    std::vector<std::array<size_t, N_POOLS>> pool_at(n_pics);
+    std::vector<std::array<int, RC_NUM>> job_at(n_pics);
+    std::vector<size_t> tb_at(n_pics), nf_at(n_pics);
+    {
+        size_t pf[N_POOLS];
+        std::copy(pool_base, pool_base + N_POOLS, pf);
+        int jf[RC_NUM] = {};
+        size_t tf = 0, nf = 0;
+        for (int i = 0; i < n_pics; ++i) {
+            for (int c = 0; c < N_POOLS; ++c) { pool_at[i][c] = pf[c]; pf[c] += cnt_pool[i][c]; }
+            for (int c = 0; c < RC_NUM; ++c) { job_at[i][c] = jf[c]; jf[c] += cnt_job[i][c]; }
+            tb_at[i] = tf;
+            tf += pics[i].n_tbs;
+            nf_at[i] = nf;
+            nf += pics[i].nofilter ? 1 : 0;
+        }
+    }
+    parallel_for(n_pics, [&](int i) {
         const p265r_picture& pic = pics[i];
         std::memcpy(h_ctus + (size_t)i * nc, pic.ctus, sizeof(p265r_ctu) * nc);
-        p265r_tb* tb_dst = h_tbs + tb_fill;
+        p265r_tb* tb_dst = h_tbs + tb_at[i];
+        size_t pool_fill[N_POOLS];
+        int job_fill[RC_NUM];
+        for (int c = 0; c < N_POOLS; ++c) pool_fill[c] = pool_at[i][c];
+        for (int c = 0; c < RC_NUM; ++c) job_fill[c] = job_at[i][c];
         for (uint32_t t = 0; t < pic.n_tbs; ++t) {
             p265r_tb tb = pic.tbs[t];
             if (tb.flags & (P265R_TB_CBF | P265R_TB_PCM)) {
@@ -407,8 +491,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         }
         DevPic& dp = b->h_pics[i];
         dp.ctus = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus) + (size_t)i * nc;
-        dp.tbs = reinterpret_cast<const p265r_tb*>(dbase + o_tbs) + tb_fill;
-        dp.jobs = reinterpret_cast<IntraJob*>(dbase + o_ijobs) + tb_fill;
+        dp.tbs = reinterpret_cast<const p265r_tb*>(dbase + o_tbs) + tb_at[i];
+        dp.jobs = reinterpret_cast<IntraJob*>(dbase + o_ijobs) + tb_at[i];
         dp.jcount = reinterpret_cast<uint32_t*>(dbase + o_jcount) + (size_t)i * nc;
         unsigned char* rec = dbase + o_rec + pic_plane_bytes * i;
         dp.rec[0] = rec;
@@ -424,24 +508,47 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
             for (int c = 0; c < 3; ++c) dp.out[c] = dp.rec[c];
         }
         if (pic.nofilter) {
-            std::memcpy(host.data() + o_nf + nf_fill * nf_bytes, pic.nofilter, nf_bytes);
-            dp.nofilter = dbase + o_nf + nf_fill * nf_bytes;
-            ++nf_fill;
+            std::memcpy(host + s_nf + nf_at[i] * nf_bytes, pic.nofilter, nf_bytes);
+            dp.nofilter = dbase + o_nf + nf_at[i] * nf_bytes;
         } else {
             dp.nofilter = nullptr;
         }
-        tb_fill += pic.n_tbs;
+    });
+    std::memcpy(host + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
+    std::memset(host + o_err, 0, o_ctus - o_err);                                        // error word
+    // alignment gaps between the arrays: zero, as the device image always had them
+    {
+        const size_t pics_end = o_pics + sizeof(DevPic) * n_pics;
+        const size_t ctus_end = o_ctus + sizeof(p265r_ctu) * nc * (size_t)n_pics;
+        const size_t tbs_end = o_tbs + sizeof(p265r_tb) * n_tbs_total;
+        std::memset(host + pics_end, 0, o_err - pics_end);
+        std::memset(host + ctus_end, 0, o_tbs - ctus_end);
+        std::memset(host + tbs_end, 0, o_pool - tbs_end);
+        for (int c = 0; c < RC_NUM; ++c) {
+            const size_t je = o_jobs[c] + sizeof(ResJob) * n_jobs[c];
+            const size_t next_start = c + 1 < RC_NUM ? o_jobs[c + 1] : o_ijobs;
+            std::memset(host + s_jobs + (je - o_jobs[0]), 0, next_start - je);
+        }
     }
-    std::memcpy(host.data() + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
-    e = hipMemcpy(b->mem, host.data(), o_rec, hipMemcpyHostToDevice);
-    if (e != hipSuccess) { int rc = hip_fail(e, "hipMemcpy(upload)"); (void)hipFree(b->mem); delete b; return rc; }
-    if (recon_input) {
+    std::memset(host + o_pool + sizeof(int16_t) * pool_total, 0, o_res - o_pool - sizeof(int16_t) * pool_total);  // pool pad
+    // device image: host-filled ranges copied, everything else of [0, o_rec) zero -- stream
+    // ordered behind any earlier work on the reused allocation, complete before returning
+    // (the staging buffer is refilled by the next upload)
+    hipStream_t st = ctx->stream;
+    e = hipMemcpyAsync(dbase, host, o_res, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemsetAsync(dbase + o_res, 0, o_jobs[0] - o_res, st);
+    if (e == hipSuccess && jobs_bytes) e = hipMemcpyAsync(dbase + o_jobs[0], host + s_jobs, jobs_bytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemsetAsync(dbase + o_ijobs, 0, o_rec - o_ijobs, st);
+    if (e == hipSuccess && n_nf) e = hipMemcpyAsync(dbase + o_nf, host + s_nf, nf_bytes * n_nf, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && recon_input) {
         const int wd[3] = {g.w, g.cw, g.cw}, ht[3] = {g.h, g.ch, g.ch};
         for (int i = 0; i < n_pics && e == hipSuccess; ++i)
             for (int c = 0; c < 3 && e == hipSuccess; ++c)
-                e = hipMemcpy2D(b->h_pics[i].rec[c], g.stride[c], pics[i].recon[c], wd[c], wd[c], ht[c], hipMemcpyHostToDevice);
-        if (e != hipSuccess) { int rc = hip_fail(e, "hipMemcpy2D(recon input)"); (void)hipFree(b->mem); delete b; return rc; }
+                e = hipMemcpy2DAsync(b->h_pics[i].rec[c], g.stride[c], pics[i].recon[c], wd[c], wd[c], ht[c],
+                                     hipMemcpyHostToDevice, st);
     }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { int rc = hip_fail(e, "upload"); (void)hipFree(b->mem); delete b; return rc; }
     *out = b;
     return P265R_OK;
 }
@@ -577,7 +684,18 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (ctx->pending == b) ctx->pending = nullptr;
-    hipError_t e = b->mem ? hipFree(b->mem) : hipSuccess;
+    hipError_t e = hipSuccess;
+    if (b->mem) {
+        // keep the larger of (cache, this allocation) for the next upload; callers free a batch
+        // only once its work is complete (download/sync), and reuse is ordered on ctx->stream
+        if (!ctx->cache_mem || b->bytes > ctx->cache_bytes) {
+            if (ctx->cache_mem) e = hipFree(ctx->cache_mem);
+            ctx->cache_mem = b->mem;
+            ctx->cache_bytes = b->bytes;
+        } else {
+            e = hipFree(b->mem);
+        }
+    }
     delete b;
     return e == hipSuccess ? P265R_OK : hip_fail(e, "hipFree");
 }

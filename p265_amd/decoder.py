@@ -10,6 +10,8 @@ stream's decoded-picture-hash SEI when present (D.3.19).
 
 No CPU reconstruction exists on this path: a missing library or GPU raises.
 """
+import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -57,10 +59,15 @@ def _batches(items, key, size):
 
 def decode_bytes(data: bytes, device: int = 0, batch: int = 64, threads: int = 0,
                  verify_hash: bool = True) -> List[DecodedFrame]:
-    """Decode a whole stream; returns the output pictures in output order."""
+    """Decode a whole stream; returns the output pictures in output order.
+
+    Picture hashes are computed on host threads (the C hash releases the GIL) while the
+    next batch decodes on the GPU."""
     pics = bitstream.decode_stream(data, threads=threads)
     frames = []
     contexts = {}
+    pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
+    checks = []
     try:
         for group in _batches(list(enumerate(pics)), lambda it: it[1].params.tobytes(), batch):
             key = group[0][1].params.tobytes()
@@ -69,15 +76,18 @@ def decode_bytes(data: bytes, device: int = 0, batch: int = 64, threads: int = 0
                 ctx = contexts[key] = recon.ReconContext(group[0][1].params, device=device)
             outs = ctx.decode([d.picture for _, d in group])
             for (i, d), planes in zip(group, outs):
-                ok = None
+                fr = DecodedFrame(poc=d.poc, output_rank=d.output_rank, decode_index=i,
+                                  planes=planes, crop=tuple(int(v) for v in d.crop), hash_ok=None)
                 if d.hash is not None:
-                    ok = all(bitstream.plane_hash(planes[c], d.hash_type) == d.hash[c] for c in range(3))
-                    if verify_hash and not ok:
-                        raise HashMismatch("picture %d (POC %d): decoded picture hash SEI mismatch" % (i, d.poc))
+                    checks.append((fr, d, [pool.submit(bitstream.plane_hash, planes[c], d.hash_type) for c in range(3)]))
                 if d.output_rank >= 0:
-                    frames.append(DecodedFrame(poc=d.poc, output_rank=d.output_rank, decode_index=i,
-                                               planes=planes, crop=tuple(int(v) for v in d.crop), hash_ok=ok))
+                    frames.append(fr)
+        for fr, d, futs in checks:
+            fr.hash_ok = all(f.result() == d.hash[c] for c, f in enumerate(futs))
+            if verify_hash and not fr.hash_ok:
+                raise HashMismatch("picture %d (POC %d): decoded picture hash SEI mismatch" % (fr.decode_index, d.poc))
     finally:
+        pool.shutdown(wait=True)
         for ctx in contexts.values():
             ctx.close()
     frames.sort(key=lambda f: f.output_rank)
