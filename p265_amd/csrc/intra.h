@@ -37,7 +37,7 @@ struct DevPic {                 // per picture, device-resident table
     uint8_t* out[3];            // SAO output planes (== rec when SAO is off)
     const uint8_t* nofilter;    // per 8x8 luma block or nullptr
     IntraJob* jobs;             // same index space as tbs (jobs of a CTU start at tb_begin)
-    uint32_t* jcount;           // per CTU: number of jobs
+    uint32_t* jcount;           // per CTU: luma jobs | chroma jobs << 16 (luma listed first)
     uint8_t* dbk_map;           // per 8x8 luma block (loopfilter.h), nullptr without deblocking
 };
 

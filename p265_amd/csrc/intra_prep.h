@@ -68,7 +68,18 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const p265r_tb* tbs = P.tbs + me.tb_begin;
     IntraJob* jobs = P.jobs + me.tb_begin;
     const int cnt = me.tb_count;
-    int out = 0;
+    // luma jobs first (decode order), then the chroma jobs (Cb+Cr pairs, unpaired Cb / Cr, in
+    // decode order): the row kernel runs the two components as independent row chains
+    // (4:2:0 intra prediction never reads across components)
+    int n_luma = 0;
+    for (int base = 0; base < cnt; base += 64) {
+        const int t = base + lane;
+        n_luma += __popcll(__ballot(t < cnt && tbs[t].c_idx == 0));
+    }
+    int out_l = 0, out_c = n_luma;
+    auto rank = [&](unsigned long long m) {
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
     for (int base = 0; base < cnt; base += 64) {
         const int t = base + lane;
         const bool valid = t < cnt;
@@ -78,9 +89,11 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         if (valid && t + 1 < cnt) next = tbs[t + 1];
         const bool cr_taken = valid && t > 0 && tb_same_tu_chroma(prev, rec);
         const bool keep = valid && !cr_taken;
-        const unsigned long long km = __ballot(keep);
-        const int slot = out + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
-        out += __popcll(km);
+        const bool kl = keep && rec.c_idx == 0;
+        const unsigned long long ml = __ballot(kl), mc = __ballot(keep && !kl);
+        const int slot = kl ? out_l + rank(ml) : out_c + rank(mc);
+        out_l += __popcll(ml);
+        out_c += __popcll(mc);
         if (keep) {
             const int lg = rec.log2_size, n = 1 << lg, c = rec.c_idx;
             const int sub = c ? 1 : 0;
@@ -142,7 +155,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
         }
     }
-    if (lane == 0) P.jcount[addr] = (uint32_t)out;
+    if (lane == 0) P.jcount[addr] = (uint32_t)out_l | (uint32_t)(out_c - n_luma) << 16;
 }
 
 }  // namespace p265r

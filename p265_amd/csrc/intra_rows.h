@@ -1,8 +1,9 @@
 // Intra prediction + reconstruction, CU-local wavefront ("row pipeline") schedule.
 //
-// One workgroup owns whole pictures: its W waves pull CTU ROWS from an LDS row queue
-// (pictures of the workgroup in order, rows top to bottom) and walk each row left to
-// right.  Row r may start CTU cx once row r-1 has finished CTU min(cx+2, wc) - the
+// One workgroup owns whole pictures: its W waves pull CTU ROW UNITS from an LDS row queue
+// (pictures of the workgroup in order, rows top to bottom; every CTU row is two units, the
+// luma chain and the chroma (Cb + Cr) chain, which 4:2:0 intra prediction never couples)
+// and walk each unit left to right.  Row r may start CTU cx once row r-1 has finished CTU min(cx+2, wc) - the
 // 2-CTU lag that makes the left, top-left, top and top-right CTUs available.  The
 // queue runs across picture boundaries, so waves never idle at a picture's ramp-down;
 // picture slots (line buffers + progress words) are reused only after the slot's
@@ -520,7 +521,8 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
     RowCtrl& ctl = *reinterpret_cast<RowCtrl*>(smem);
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int prog_bytes = (fs_count * g.hc * 4 + 15) & ~15;
+    const int units = 2 * g.hc;                       // row units per picture: (cy, luma), (cy, chroma)
+    const int prog_bytes = (fs_count * units * 4 + 15) & ~15;
     int* prog = reinterpret_cast<int*>(smem + 256);
     WaveLds& L = reinterpret_cast<WaveLds*>(smem + 256 + prog_bytes)[wave];
     const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
@@ -528,13 +530,13 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
 
     if (threadIdx.x == 0) { ctl.next_row = 0; ctl.error = 0; }
     if (threadIdx.x < 32) ctl.done[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < fs_count * g.hc; i += 64 * W) prog[i] = -1;
+    for (int i = threadIdx.x; i < fs_count * units; i += 64 * W) prog[i] = -1;
     __syncthreads();
 
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int n_my = b < n_pics ? (n_pics - b + G - 1) / G : 0;
-    const int rows_total = n_my * g.hc;
+    const int rows_total = n_my * units;
     const int ctb = 1 << g.ctb_log2;
     // bounded spin-wait on an LDS word; false = gave up (error published, caller bails out).
     // Every condition is made wave-uniform (readfirstlane) so the loops are scalar loops.
@@ -563,7 +565,8 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         r = __builtin_amdgcn_readfirstlane(r);
         if (r >= rows_total || failed) break;
         P265R_TRACE(2 | (r << 8));
-        const int j = r / g.hc, cy = r - j * g.hc;
+        const int j = r / units, rem = r - j * units;
+        const int cy = rem >> 1, comp = rem & 1;          // 0: luma chain, 1: chroma (Cb + Cr) chain
         const int slot = j % fs_count, gen = j / fs_count;
         const DevPic* Pp = pics + b + j * G;
         const p265r_ctu* ctus = uniform(gload(&Pp->ctus));
@@ -573,13 +576,13 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         // slot's previous occupant) has completed all its rows; those rows were dequeued
         // earlier and are held by running waves, so this wait always ends.
         if (!wait_until([&] {
-                return __hip_atomic_load(&ctl.done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen * g.hc;
+                return __hip_atomic_load(&ctl.done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen * units;
             })) { failed = true; break; }
         P265R_TRACE(3 | (r << 8));
         unsigned char* line_cur = lines + (size_t)(slot * 2 + (cy & 1)) * line_bytes;
         const unsigned char* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
-        int* my_prog = &prog[slot * g.hc + cy];
-        const int* up_prog = &prog[slot * g.hc + (cy > 0 ? cy - 1 : 0)];
+        int* my_prog = &prog[(slot * g.hc + cy) * 2 + comp];
+        const int* up_prog = &prog[(slot * g.hc + (cy > 0 ? cy - 1 : 0)) * 2 + comp];
         const int tag = (j & 0xffff) << 16;
         __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 
@@ -597,8 +600,11 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             const int addr = cy * g.wc + cx;
             // this CTU's job list (intra_prep_kernel): first job = its first TB index
             const uint32_t tb_begin = uniform(gload(reinterpret_cast<const uint2*>(ctus + addr))).x;
-            const int nt = (int)__builtin_amdgcn_readfirstlane(*gptr(jcount + addr));
-            const IntraJob* jl = jobs + tb_begin;
+            // job counts: luma in bits 0..15 (listed first), chroma in bits 16..31 (intra_prep.h)
+            const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(*gptr(jcount + addr));
+            const int n_luma = (int)(jc & 0xffffu);
+            const int nt = comp ? (int)(jc >> 16) : n_luma;
+            const IntraJob* jl = jobs + tb_begin + (comp ? n_luma : 0);
             // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr)
             const uint8_t* ltop_l = line_up + x0;
             const uint8_t* ltop_c = line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
@@ -704,6 +710,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             // ---- publish the CTU: planes (HBM), bottom line (LDS), right column (LDS) ----------
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
+                if ((c == 0) != (comp == 0)) continue;          // this chain's planes only (wave-uniform)
                 const int sub = c ? 1 : 0;
                 const int cs = ctb >> sub;
                 const int Wd = c ? g.cw : g.w, Ht = c ? g.ch : g.h;

@@ -178,9 +178,9 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
     // picture slots: the W rows in flight are consecutive in the queue, so they span at
     // most ceil(W / hc) + 1 pictures; a slot is reused only after its previous picture is
     // complete (the kernel waits for that, so fewer slots would still be correct)
-    int fs = std::min(32, (W + g.hc - 1) / g.hc + 1);
+    int fs = std::min(32, (W + 2 * g.hc - 1) / (2 * g.hc) + 1);     // 2 row units (luma, chroma) per CTU row
     auto lds_of = [&](int f) {
-        return 256 + (size_t)((f * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
+        return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
     const size_t lds = lds_of(fs);
