@@ -30,6 +30,7 @@ struct Sps {
     int conf_left = 0, conf_right = 0, conf_top = 0, conf_bottom = 0;   // in chroma units (7.4.3.2.1)
     int bit_depth_y = 8, bit_depth_c = 8;
     int log2_max_poc_lsb = 4;
+    int max_num_reorder = 0;          // sps_max_num_reorder_pics[sps_max_sub_layers_minus1] (C.5.2.2 bumping)
     int log2_min_cb = 3, log2_ctb = 4, log2_min_tb = 2, log2_max_tb = 5;
     int max_th_depth_inter = 0, max_th_depth_intra = 0;
     int scaling_list_enabled = 0;

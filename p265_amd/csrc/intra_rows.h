@@ -508,7 +508,7 @@ template <int W>
 __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
                                                            const int16_t* __restrict__ resid,
-                                                           Geo g, int n_pics, int fs_count,
+                                                           Geo g, int n_pics, int fs_count, int lead,
                                                            int* __restrict__ err_flag,
                                                            int* __restrict__ dbg) {
     // debug trace (P265R_DEBUG_SYNC=1): host-mapped words, one per wave
@@ -566,7 +566,20 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         if (r >= rows_total || failed) break;
         P265R_TRACE(2 | (r << 8));
         const int j = r / units, rem = r - j * units;
-        const int cy = rem >> 1, comp = rem & 1;          // 0: luma chain, 1: chroma (Cb + Cr) chain
+        // queue order inside a picture: the luma chain (the longer one) leads by `lead` rows:
+        // L0 .. L(d-1), then L(d) C0 L(d+1) C1 ..., then the remaining chroma rows.  Either
+        // chain's rows stay in order, so a dequeued row's predecessor is always held by a wave.
+        int cy, comp;                                      // comp 0: luma chain, 1: chroma (Cb + Cr)
+        {
+            const int d = min(lead, g.hc);
+            if (rem < d) {
+                cy = rem; comp = 0;
+            } else {
+                const int k = rem - d, pairs = 2 * (g.hc - d);
+                if (k < pairs) { cy = (k & 1) ? (k >> 1) : d + (k >> 1); comp = k & 1; }
+                else { cy = g.hc - d + (k - pairs); comp = 1; }
+            }
+        }
         const int slot = j % fs_count, gen = j / fs_count;
         const DevPic* Pp = pics + b + j * G;
         const p265r_ctu* ctus = uniform(gload(&Pp->ctus));

@@ -87,6 +87,8 @@ struct p265r_ctx {
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
     int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16); 8 = 2 workgroups per CU
+    int luma_lead = 3;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
+                               // measured, 1080p W=8: lead 0/1/2/3/5/8/17 -> 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
     // reused across batches: pinned host staging (grow-only) and one freed device allocation
@@ -197,7 +199,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
         std::memset(dbg, 0, sizeof(int) * grid * W * 3);
         fprintf(stderr, "[p265r] rows kernel W=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, grid, lds, fs, per_cu);
     }
-    fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, b->d_err, dbg);
+    fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
     HIP_TRY(hipGetLastError());
     if (dbg) {
         for (int it = 0; it < 100; ++it) {
@@ -287,6 +289,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
+    if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 8 || w == 16) ctx->row_waves = w;
