@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define P265FE_ABI_VERSION 1u
+#define P265FE_ABI_VERSION 2u
 
 #define P265FE_OK            0
 #define P265FE_EINVAL       -1   /* bad argument                                   */
@@ -55,6 +55,9 @@ extern "C" {
 #define P265FE_HASH_MD5       0
 #define P265FE_HASH_CRC       1
 #define P265FE_HASH_CHECKSUM  2
+
+/* p265fe_feed flags */
+#define P265FE_FLUSH          1   /* end of stream: the last access unit is complete */
 
 typedef struct p265fe_picture_info {
     p265r_params     params;        /* back-end parameters of this picture's SPS/PPS         */
@@ -73,7 +76,13 @@ typedef struct p265fe_picture_info {
     uint16_t         n_slices;      /* slice segments                                        */
     uint32_t         n_cus;         /* coding units parsed                                   */
     uint8_t          hash[3][16];   /* decoded picture hash per component (MD5: 16 B, CRC: 2 B BE, checksum: 4 B BE) */
+    int32_t          cvs_id;        /* coded video sequence counter (IRAP with NoRaslOutputFlag = 1) */
+    uint8_t          max_num_reorder; /* sps_max_num_reorder_pics: output "bumping" (C.5.2.2)   */
+    uint8_t          output_flag;   /* PicOutputFlag                                             */
+    uint16_t         reserved;
 } p265fe_picture_info;
+
+typedef struct p265fe_pictures p265fe_pictures;
 
 typedef struct p265fe_decoder p265fe_decoder;
 
@@ -88,6 +97,20 @@ int  p265fe_decode(p265fe_decoder* dec, const uint8_t* data, size_t size, int n_
 
 /* Picture i (decode order) of the last p265fe_decode. */
 int  p265fe_picture(p265fe_decoder* dec, int i, p265fe_picture_info* out);
+
+/* Streaming.  Feed the byte stream in order, in chunks of any size (flags = P265FE_FLUSH
+ * with the last one, which may be empty).  Parameter sets, POC state, the access unit being
+ * assembled and an incomplete trailing NAL unit carry over between calls; access units that
+ * are complete (the next access unit has started, or FLUSH) are parsed on n_threads workers
+ * and queued.  Returns the number of queued pictures, or an error code.  (p265fe_decode
+ * resets this state.) */
+int  p265fe_feed(p265fe_decoder* dec, const uint8_t* data, size_t size, int n_threads, int flags);
+/* Move the queued pictures (decode order) into a new set owned by the caller; returns its
+ * size.  output_rank is -1 in a set: output order is the caller's (cvs_id, poc,
+ * max_num_reorder, output_flag give what the bumping process needs). */
+int  p265fe_take(p265fe_decoder* dec, p265fe_pictures** out);
+int  p265fe_pictures_get(const p265fe_pictures* set, int i, p265fe_picture_info* out);
+void p265fe_pictures_free(p265fe_pictures* set);
 
 /* Decoded picture hash (D.3.19) of one 8-bit sample plane (width x height, row stride in
  * bytes): P265FE_HASH_MD5 -> 16 bytes, _CRC -> 2 bytes big-endian, _CHECKSUM -> 4 bytes

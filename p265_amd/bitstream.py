@@ -5,10 +5,14 @@ ctu.py / cu.py / tu.py / sao.py with the CABAC engine of cabac.py) for all-intra
 streams.  ``decode_stream(data)`` parses a whole Annex-B byte stream on host threads
 and returns, per picture in decode order, the back-end records that the reference's
 per-CU hook would have produced (``records.Picture``) plus the picture's params,
-POC, output rank, conformance window and decoded-picture hash.
+POC, output rank, conformance window and decoded-picture hash.  ``StreamParser``
+does the same incrementally: ``feed()`` arbitrary chunks, get the pictures completed
+so far (bounded memory for arbitrarily long streams).
 
-There is no fallback: a missing library raises ``LibraryNotFound``; a malformed or
-unsupported stream raises ``BitstreamError`` / ``UnsupportedStream``.
+The record arrays are read-only zero-copy views of buffers the library owns; they
+keep those buffers alive.  There is no fallback: a missing library raises
+``LibraryNotFound``; a malformed or unsupported stream raises ``BitstreamError`` /
+``UnsupportedStream``.
 """
 import ctypes
 import os
@@ -24,8 +28,10 @@ from . import records as R
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("P265FE_LIB", os.path.join(HERE, "libp265fe.so"))
 
+ABI_VERSION = 2
 OK, EINVAL, ENOMEM, EUNSUPPORTED, EBITSTREAM = 0, -1, -2, -4, -8
 HASH_NONE, HASH_MD5, HASH_CRC, HASH_CHECKSUM = -1, 0, 1, 2
+FLUSH = 1
 
 
 class BitstreamError(ValueError):
@@ -43,7 +49,8 @@ class PictureInfoC(ctypes.Structure):
                 ("output_rank", ctypes.c_int32), ("crop_left", ctypes.c_uint16), ("crop_right", ctypes.c_uint16),
                 ("crop_top", ctypes.c_uint16), ("crop_bottom", ctypes.c_uint16), ("nal_unit_type", ctypes.c_uint8),
                 ("hash_type", ctypes.c_int8), ("n_slices", ctypes.c_uint16), ("n_cus", ctypes.c_uint32),
-                ("hash", (ctypes.c_uint8 * 16) * 3)]
+                ("hash", (ctypes.c_uint8 * 16) * 3), ("cvs_id", ctypes.c_int32),
+                ("max_num_reorder", ctypes.c_uint8), ("output_flag", ctypes.c_uint8), ("reserved", ctypes.c_uint16)]
 
 
 _vp = ctypes.c_void_p
@@ -52,6 +59,10 @@ SIGNATURES = {
     "p265fe_destroy": (None, [_vp]),
     "p265fe_decode": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]),
     "p265fe_picture": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PictureInfoC)]),
+    "p265fe_feed": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
+    "p265fe_take": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "p265fe_pictures_get": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PictureInfoC)]),
+    "p265fe_pictures_free": (None, [_vp]),
     "p265fe_last_error": (ctypes.c_char_p, [_vp]),
     "p265fe_abi_version": (ctypes.c_uint32, []),
     "p265fe_plane_hash": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -72,8 +83,8 @@ def load():
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.restype, fn.argtypes = res, args
-            if lib.p265fe_abi_version() != 1:
-                raise _lib.LibraryNotFound("libp265fe.so ABI version mismatch")
+            if lib.p265fe_abi_version() != ABI_VERSION:
+                raise _lib.LibraryNotFound("libp265fe.so ABI version mismatch (rebuild)")
             _handle = lib
         return _handle
 
@@ -84,23 +95,20 @@ class DecodedPicture:
     params: np.ndarray
     picture: R.Picture
     poc: int
-    output_rank: int            # -1: not output (pic_output_flag 0 / RASL after a CRA start)
+    output_rank: int            # decode_stream: rank in output order (-1: not output); StreamParser: -1
     crop: tuple                 # conformance window (left, right, top, bottom) in luma samples
     nal_unit_type: int
     n_slices: int
     n_cus: int
     hash_type: int
     hash: Optional[list]        # per component bytes of the decoded picture hash SEI
-
-
-def _params_np(pc):
-    kw = {name: getattr(pc, name) for name, _ in _lib.Params._fields_ if name not in ("version", "reserved")}
-    return R.make_params(**kw)
+    cvs_id: int = 0             # coded video sequence (IRAP with NoRaslOutputFlag) counter
+    max_num_reorder: int = 0    # sps_max_num_reorder_pics of its SPS (output bumping, C.5.2.2)
+    output_flag: bool = True    # PicOutputFlag
 
 
 class _Owner:
-    """Keeps one p265fe_decoder (and so the record buffers it owns) alive while any array
-    viewing those buffers is alive; destroys it when the last view goes away."""
+    """Destroys one p265fe_decoder when the last object referring to it goes away."""
 
     def __init__(self, lib, handle):
         self.lib, self.handle = lib, handle
@@ -111,8 +119,25 @@ class _Owner:
             self.handle = None
 
 
+class _SetOwner:
+    """Frees one p265fe_pictures set when the last record array viewing it goes away."""
+
+    def __init__(self, lib, handle):
+        self.lib, self.handle = lib, handle
+
+    def __del__(self):
+        if self.handle:
+            self.lib.p265fe_pictures_free(self.handle)
+            self.handle = None
+
+
+def _params_np(pc):
+    kw = {name: getattr(pc, name) for name, _ in _lib.Params._fields_ if name not in ("version", "reserved")}
+    return R.make_params(**kw)
+
+
 def _view(ptr, n, dtype, owner):
-    """Zero-copy numpy view of a decoder-owned buffer (no first-touch copy of the records)."""
+    """Zero-copy numpy view of a library-owned buffer (no first-touch copy of the records)."""
     if n == 0:
         return np.zeros(0, dtype)
     buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
@@ -131,28 +156,19 @@ def plane_hash(plane, hash_type):
     return out.raw[:{HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}[int(hash_type)]]
 
 
-def decode_stream(data: bytes, threads: int = 0, validate: bool = False):
-    """Parse an Annex-B HEVC byte stream; returns [DecodedPicture] in decode order.
+def _fail(lib, h, n, what):
+    msg = lib.p265fe_last_error(h).decode(errors="replace")
+    cls = UnsupportedStream if n == EUNSUPPORTED else BitstreamError
+    raise cls("%s: %s (%d)" % (what, msg, n))
 
-    The record arrays are read-only views of the decoder's buffers (kept alive by the
-    arrays).  ``validate`` re-runs the host-side record checks (the back-end's upload
-    validates every record again in C++ before any kernel sees it)."""
-    lib = load()
-    h = ctypes.c_void_p()
-    if lib.p265fe_create(ctypes.byref(h)) != OK:
-        raise MemoryError("p265fe_create failed")
-    owner = _Owner(lib, h)
-    n = lib.p265fe_decode(h, bytes(data), len(data), int(threads))
-    if n < 0:
-        msg = lib.p265fe_last_error(h).decode(errors="replace")
-        cls = UnsupportedStream if n == EUNSUPPORTED else BitstreamError
-        raise cls("p265fe_decode: %s (%d)" % (msg, n))
+
+def _collect(get, n, owner, validate, base=0):
     out = []
     info = PictureInfoC()
     for i in range(n):
-        rc = lib.p265fe_picture(h, i, ctypes.byref(info))
+        rc = get(i, ctypes.byref(info))
         if rc != OK:
-            raise BitstreamError("p265fe_picture(%d) failed (%d)" % (i, rc))
+            raise BitstreamError("picture %d: info failed (%d)" % (base + i, rc))
         params = _params_np(info.params)
         ctus = _view(info.ctus, info.n_ctus, R.CTU_DTYPE, owner)
         tbs = _view(info.tbs, info.n_tbs, R.TB_DTYPE, owner)
@@ -165,7 +181,7 @@ def decode_stream(data: bytes, threads: int = 0, validate: bool = False):
             if arr is not None:
                 arr.flags.writeable = False
         pic = R.Picture(ctus=ctus, tbs=tbs, coef=coef, nofilter=nof,
-                        meta={"poc": int(info.poc), "decode_index": i})
+                        meta={"poc": int(info.poc), "decode_index": base + i})
         if validate:
             R.validate(params, pic)
         hl = {HASH_MD5: 16, HASH_CRC: 2, HASH_CHECKSUM: 4}.get(int(info.hash_type))
@@ -174,5 +190,59 @@ def decode_stream(data: bytes, threads: int = 0, validate: bool = False):
                                   output_rank=int(info.output_rank),
                                   crop=(info.crop_left, info.crop_right, info.crop_top, info.crop_bottom),
                                   nal_unit_type=int(info.nal_unit_type), n_slices=int(info.n_slices),
-                                  n_cus=int(info.n_cus), hash_type=int(info.hash_type), hash=hv))
+                                  n_cus=int(info.n_cus), hash_type=int(info.hash_type), hash=hv,
+                                  cvs_id=int(info.cvs_id), max_num_reorder=int(info.max_num_reorder),
+                                  output_flag=bool(info.output_flag)))
     return out
+
+
+def decode_stream(data: bytes, threads: int = 0, validate: bool = False):
+    """Parse a whole Annex-B HEVC byte stream; returns [DecodedPicture] in decode order.
+
+    ``validate`` re-runs the host-side record checks (the back-end's upload validates
+    every record again in C++ before any kernel sees it)."""
+    lib = load()
+    h = ctypes.c_void_p()
+    if lib.p265fe_create(ctypes.byref(h)) != OK:
+        raise MemoryError("p265fe_create failed")
+    owner = _Owner(lib, h)
+    n = lib.p265fe_decode(h, bytes(data), len(data), int(threads))
+    if n < 0:
+        _fail(lib, h, n, "p265fe_decode")
+    return _collect(lambda i, ref: lib.p265fe_picture(h, i, ref), n, owner, validate)
+
+
+class StreamParser:
+    """Incremental parsing of an Annex-B stream fed in arbitrary chunks.
+
+    ``feed(chunk)`` returns the pictures completed so far, in decode order; stream state
+    (parameter sets, POC, a partial access unit or NAL unit) carries over between calls;
+    ``feed(b"", flush=True)`` ends the stream.  Output order is the caller's (see
+    decoder.OutputQueue): ``output_rank`` stays -1 here."""
+
+    def __init__(self, threads: int = 0, validate: bool = False):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        if self.lib.p265fe_create(ctypes.byref(h)) != OK:
+            raise MemoryError("p265fe_create failed")
+        self._owner = _Owner(self.lib, h)
+        self.h = h
+        self.threads = int(threads)
+        self.validate = validate
+        self.n_pictures = 0
+
+    def feed(self, data: bytes, flush: bool = False):
+        lib = self.lib
+        data = bytes(data)
+        n = lib.p265fe_feed(self.h, data, len(data), self.threads, FLUSH if flush else 0)
+        if n < 0:
+            _fail(lib, self.h, n, "p265fe_feed")
+        sp = ctypes.c_void_p()
+        cnt = lib.p265fe_take(self.h, ctypes.byref(sp))
+        if cnt < 0:
+            raise MemoryError("p265fe_take failed (%d)" % cnt)
+        owner = _SetOwner(lib, sp)
+        pics = _collect(lambda i, ref: lib.p265fe_pictures_get(sp, i, ref), cnt, owner, self.validate,
+                        base=self.n_pictures)
+        self.n_pictures += cnt
+        return pics

@@ -1,7 +1,9 @@
 // C ABI of the native front-end (include/p265fe.h): NAL dispatch in stream order
-// (dec.py:18-64, nalu.py:88-131), picture order count (8.3.1), output order, decoded
-// picture hash SEI (D.2.20; nalu.py:130 raises on SEI), and parallel slice-data parsing of
-// independent all-intra pictures on worker threads.
+// (dec.py:18-64, nalu.py:88-131), access-unit assembly, picture order count (8.3.1),
+// decoded picture hash SEI (D.2.20; nalu.py:130 raises on SEI), and parallel slice-data
+// parsing of independent all-intra pictures on worker threads.  Streams can be fed in
+// arbitrary chunks (p265fe_feed / p265fe_take): parameter sets, POC state, the picture
+// being assembled and an incomplete trailing NAL unit carry over between calls.
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -21,7 +23,7 @@ namespace {
 
 struct PictureJob {
     std::shared_ptr<const Active> act;
-    std::vector<size_t> nal_idx;            // slice segment NAL units, decode order
+    std::vector<Nal> slices;                // slice segment NAL units, decode order
     std::vector<std::unique_ptr<SliceHeader>> hdrs;
     int poc = 0, nal_type = 0, output = 1, cvs = 0;
     int hash_type = P265FE_HASH_NONE;
@@ -31,6 +33,8 @@ struct PictureJob {
 
 bool is_irap(int t) { return t >= 16 && t <= 23; }
 bool is_vcl_supported(int t) { return (t >= 0 && t <= 9) || (t >= 16 && t <= 21); }
+// NAL unit types that start a new access unit (7.4.2.4.4) besides a first slice segment
+bool starts_access_unit(int t) { return (t >= 32 && t <= 35) || t == 39 || (t >= 41 && t <= 44) || (t >= 48 && t <= 55); }
 
 // decoded_picture_hash (D.2.20) from an SEI RBSP (7.3.5); returns true if found
 bool parse_picture_hash(const std::vector<uint8_t>& rbsp, int chroma_format_idc, PictureJob& job) {
@@ -60,12 +64,32 @@ bool parse_picture_hash(const std::vector<uint8_t>& rbsp, int chroma_format_idc,
     return false;
 }
 
+// Stream-order state that survives between p265fe_feed calls.
+struct StreamState {
+    std::shared_ptr<Sps> sps_tab[16];
+    std::shared_ptr<Pps> pps_tab[64];
+    std::shared_ptr<const Active> cached;
+    const Sps* cached_sps = nullptr;
+    const Pps* cached_pps = nullptr;
+    std::unique_ptr<PictureJob> cur;          // access unit being assembled
+    const SliceHeader* prev_indep = nullptr;  // into cur->hdrs
+    bool first_pic = true, after_eos = false, no_rasl_output = false;
+    int prev_tid0_poc = 0, cvs = -1;
+    std::vector<uint8_t> tail;                // from the last start code of the previous feed
+    std::vector<std::unique_ptr<PictureJob>> complete;   // assembled, slice data not parsed yet
+};
+
 }  // namespace
 
-struct p265fe_decoder {
-    std::vector<Nal> nals;
+struct p265fe_pictures {
     std::vector<std::unique_ptr<PictureJob>> jobs;
     std::vector<PictureRecords> recs;
+};
+
+struct p265fe_decoder {
+    StreamState st;
+    p265fe_pictures ready;                    // parsed, not yet taken
+    p265fe_pictures* last = nullptr;          // result of p265fe_decode (p265fe_picture)
     std::string err;
 };
 
@@ -74,194 +98,153 @@ static int set_err(p265fe_decoder* d, int code, const std::string& msg) {
     return code;
 }
 
-extern "C" {
+namespace {
 
-uint32_t p265fe_abi_version(void) { return P265FE_ABI_VERSION; }
-
-int p265fe_create(p265fe_decoder** out) {
-    if (!out) return P265FE_EINVAL;
-    try {
-        *out = new p265fe_decoder();
-    } catch (...) {
-        return P265FE_ENOMEM;
-    }
-    return P265FE_OK;
+void finish_current(StreamState& st) {
+    if (st.cur) st.complete.push_back(std::move(st.cur));
+    st.cur.reset();
+    st.prev_indep = nullptr;
 }
 
-void p265fe_destroy(p265fe_decoder* d) { delete d; }
-
-const char* p265fe_last_error(p265fe_decoder* d) { return d ? d->err.c_str() : ""; }
-
-int p265fe_decode(p265fe_decoder* d, const uint8_t* data, size_t size, int n_threads) {
-    if (!d || (!data && size)) return P265FE_EINVAL;
-    d->err.clear();
-    d->jobs.clear();
-    d->recs.clear();
-    try {
-        d->nals = split_nals(data, size);
-        // ---- pass 1 (stream order): parameter sets, slice headers, POC, SEI ----
-        std::shared_ptr<Sps> sps_tab[16];
-        std::shared_ptr<Pps> pps_tab[64];
-        std::shared_ptr<const Active> cached;
-        const Sps* cached_sps = nullptr;
-        const Pps* cached_pps = nullptr;
-        PictureJob* cur = nullptr;
-        const SliceHeader* prev_indep = nullptr;
-        bool first_pic = true, after_eos = false;
-        int prev_tid0_poc = 0, cvs = -1;
-        bool no_rasl_output = false;
-        for (size_t i = 0; i < d->nals.size(); ++i) {
-            const Nal& nal = d->nals[i];
-            if (nal.layer_id != 0) continue;
-            BitReader br(nal.rbsp.data(), nal.rbsp.size());
-            if (nal.type == 32) {
-                parse_vps(br);
-            } else if (nal.type == 33) {
-                auto s = std::make_shared<Sps>(parse_sps(br));
-                sps_tab[s->sps_id] = s;
-            } else if (nal.type == 34) {
-                auto p = std::make_shared<Pps>(parse_pps(br));
-                pps_tab[p->pps_id] = p;
-            } else if (nal.type == 36 || nal.type == 37) {   // end of sequence / bitstream
-                after_eos = true;
-                cur = nullptr;
-            } else if (nal.type == 40 || nal.type == 39) {
-                if (nal.type == 40 && cur) parse_picture_hash(nal.rbsp, cur->act->sps.chroma_format_idc, *cur);
-            } else if (is_vcl_supported(nal.type)) {
-                int first_in_pic = 0;
-                int pps_id = peek_slice_pps_id(nal.rbsp, nal.type, &first_in_pic);
-                if (pps_id > 63 || !pps_tab[pps_id]) bs_fail("slice refers to a missing PPS");
-                const Pps* pps = pps_tab[pps_id].get();
-                if (!sps_tab[pps->sps_id]) bs_fail("PPS refers to a missing SPS");
-                const Sps* sps = sps_tab[pps->sps_id].get();
-                if (first_in_pic) {
-                    if (!cached || cached_sps != sps || cached_pps != pps) {
-                        cached = activate(*sps, *pps);
-                        cached_sps = sps;
-                        cached_pps = pps;
-                    }
-                    d->jobs.push_back(std::make_unique<PictureJob>());
-                    cur = d->jobs.back().get();
-                    cur->act = cached;
-                    cur->nal_type = nal.type;
-                    prev_indep = nullptr;
-                } else if (!cur) {
-                    bs_fail("slice segment without the first slice segment of its picture");
-                } else if (pps_id != cur->act->pps.pps_id) {
-                    bs_fail("slice segments of one picture refer to different PPSs");
-                }
-                auto h = std::make_unique<SliceHeader>(parse_slice_header(br, nal.type, cur->act, prev_indep));
-                if (!h->dependent) prev_indep = h.get();
-                if (first_in_pic) {
-                    // picture order count (8.3.1)
-                    int max_lsb = 1 << cur->act->sps.log2_max_poc_lsb;
-                    bool irap = is_irap(nal.type);
-                    if (irap) {
-                        no_rasl_output = (nal.type >= 16 && nal.type <= 20) || first_pic || after_eos;
-                        if (no_rasl_output) ++cvs;
-                    } else if (first_pic) {
-                        bs_fail("stream does not start with an IRAP picture");
-                    }
-                    int lsb = (nal.type == 19 || nal.type == 20) ? 0 : h->poc_lsb;
-                    int msb;
-                    if (irap && no_rasl_output) {
-                        msb = 0;
-                    } else {
-                        int prev_lsb = prev_tid0_poc & (max_lsb - 1);
-                        int prev_msb = prev_tid0_poc - prev_lsb;
-                        if (lsb < prev_lsb && prev_lsb - lsb >= max_lsb / 2) msb = prev_msb + max_lsb;
-                        else if (lsb > prev_lsb && lsb - prev_lsb > max_lsb / 2) msb = prev_msb - max_lsb;
-                        else msb = prev_msb;
-                    }
-                    cur->poc = msb + lsb;
-                    cur->cvs = cvs;
-                    bool rasl = nal.type == 8 || nal.type == 9, radl = nal.type == 6 || nal.type == 7;
-                    bool slnr = nal.type <= 14 && (nal.type % 2) == 0;
-                    if (nal.temporal_id == 0 && !rasl && !radl && !slnr) prev_tid0_poc = cur->poc;
-                    cur->output = (rasl && no_rasl_output) ? 0 : h->pic_output_flag;
-                    first_pic = false;
-                    after_eos = false;
-                }
-                cur->nal_idx.push_back(i);
-                cur->hdrs.push_back(std::move(h));
+// Stream-order processing of one complete NAL unit.
+void process_nal(StreamState& st, Nal&& nal) {
+    if (nal.layer_id != 0) return;
+    const int t = nal.type;
+    if (starts_access_unit(t)) finish_current(st);
+    BitReader br(nal.rbsp.data(), nal.rbsp.size());
+    if (t == 32) {
+        parse_vps(br);
+    } else if (t == 33) {
+        auto s = std::make_shared<Sps>(parse_sps(br));
+        st.sps_tab[s->sps_id] = s;
+    } else if (t == 34) {
+        auto p = std::make_shared<Pps>(parse_pps(br));
+        st.pps_tab[p->pps_id] = p;
+    } else if (t == 36 || t == 37) {                    // end of sequence / bitstream
+        finish_current(st);
+        st.after_eos = true;
+    } else if (t == 40) {                               // suffix SEI: belongs to the current picture
+        if (st.cur) parse_picture_hash(nal.rbsp, st.cur->act->sps.chroma_format_idc, *st.cur);
+    } else if (is_vcl_supported(t)) {
+        int first_in_pic = 0;
+        int pps_id = peek_slice_pps_id(nal.rbsp, t, &first_in_pic);
+        if (pps_id > 63 || !st.pps_tab[pps_id]) bs_fail("slice refers to a missing PPS");
+        const Pps* pps = st.pps_tab[pps_id].get();
+        if (!st.sps_tab[pps->sps_id]) bs_fail("PPS refers to a missing SPS");
+        const Sps* sps = st.sps_tab[pps->sps_id].get();
+        if (first_in_pic) {
+            finish_current(st);
+            if (!st.cached || st.cached_sps != sps || st.cached_pps != pps) {
+                st.cached = activate(*sps, *pps);
+                st.cached_sps = sps;
+                st.cached_pps = pps;
             }
+            st.cur = std::make_unique<PictureJob>();
+            st.cur->act = st.cached;
+            st.cur->nal_type = t;
+        } else if (!st.cur) {
+            bs_fail("slice segment without the first slice segment of its picture");
+        } else if (pps_id != st.cur->act->pps.pps_id) {
+            bs_fail("slice segments of one picture refer to different PPSs");
         }
-        // output order: by (coded video sequence, POC) among output pictures
-        std::vector<PictureJob*> outv;
-        for (auto& j : d->jobs)
-            if (j->output) outv.push_back(j.get());
-        std::stable_sort(outv.begin(), outv.end(), [](const PictureJob* a, const PictureJob* b) {
-            return a->cvs != b->cvs ? a->cvs < b->cvs : a->poc < b->poc;
-        });
-        for (size_t r = 0; r < outv.size(); ++r) outv[r]->output_rank = (int)r;
-
-        // ---- pass 2: slice data of independent pictures on worker threads ----
-        size_t np = d->jobs.size();
-        d->recs.resize(np);
-        int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
-        nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(np, 1));
-        std::atomic<size_t> next{0};
-        std::mutex emu;
-        int first_code = 0;
-        std::string first_msg;
-        size_t first_pic_err = (size_t)-1;
-        auto worker = [&]() {
-            for (;;) {
-                size_t k = next.fetch_add(1);
-                if (k >= np) return;
-                PictureJob& j = *d->jobs[k];
-                std::vector<SliceRef> sl;
-                for (size_t s = 0; s < j.nal_idx.size(); ++s) {
-                    const Nal& nal = d->nals[j.nal_idx[s]];
-                    sl.push_back(SliceRef{j.hdrs[s].get(), nal.rbsp.data(), nal.rbsp.size()});
-                }
-                int code = 0;
-                std::string msg;
-                try {
-                    decode_picture(*j.act, sl, d->recs[k]);
-                } catch (const Unsupported& e) {
-                    code = P265FE_EUNSUPPORTED; msg = e.what();
-                } catch (const BitstreamError& e) {
-                    code = P265FE_EBITSTREAM; msg = e.what();
-                } catch (const std::bad_alloc&) {
-                    code = P265FE_ENOMEM; msg = "out of memory";
-                } catch (const std::exception& e) {
-                    code = P265FE_EBITSTREAM; msg = e.what();
-                }
-                if (code) {
-                    std::lock_guard<std::mutex> g(emu);
-                    if (k < first_pic_err) {
-                        first_pic_err = k;
-                        first_code = code;
-                        first_msg = "picture " + std::to_string(k) + ": " + msg;
-                    }
-                }
+        PictureJob& cur = *st.cur;
+        auto h = std::make_unique<SliceHeader>(parse_slice_header(br, t, cur.act, st.prev_indep));
+        if (!h->dependent) st.prev_indep = h.get();
+        if (first_in_pic) {
+            // picture order count (8.3.1)
+            int max_lsb = 1 << cur.act->sps.log2_max_poc_lsb;
+            bool irap = is_irap(t);
+            if (irap) {
+                st.no_rasl_output = (t >= 16 && t <= 20) || st.first_pic || st.after_eos;
+                if (st.no_rasl_output) ++st.cvs;
+            } else if (st.first_pic) {
+                bs_fail("stream does not start with an IRAP picture");
             }
-        };
-        if (nt <= 1) {
-            worker();
-        } else {
-            std::vector<std::thread> th;
-            for (int t = 0; t < nt; ++t) th.emplace_back(worker);
-            for (auto& t : th) t.join();
+            int lsb = (t == 19 || t == 20) ? 0 : h->poc_lsb;
+            int msb;
+            if (irap && st.no_rasl_output) {
+                msb = 0;
+            } else {
+                int prev_lsb = st.prev_tid0_poc & (max_lsb - 1);
+                int prev_msb = st.prev_tid0_poc - prev_lsb;
+                if (lsb < prev_lsb && prev_lsb - lsb >= max_lsb / 2) msb = prev_msb + max_lsb;
+                else if (lsb > prev_lsb && lsb - prev_lsb > max_lsb / 2) msb = prev_msb - max_lsb;
+                else msb = prev_msb;
+            }
+            cur.poc = msb + lsb;
+            cur.cvs = st.cvs;
+            bool rasl = t == 8 || t == 9, radl = t == 6 || t == 7;
+            bool slnr = t <= 14 && (t % 2) == 0;
+            if (nal.temporal_id == 0 && !rasl && !radl && !slnr) st.prev_tid0_poc = cur.poc;
+            cur.output = (rasl && st.no_rasl_output) ? 0 : h->pic_output_flag;
+            st.first_pic = false;
+            st.after_eos = false;
         }
-        if (first_code) return set_err(d, first_code, first_msg);
-        return (int)np;
-    } catch (const Unsupported& e) {
-        return set_err(d, P265FE_EUNSUPPORTED, e.what());
-    } catch (const BitstreamError& e) {
-        return set_err(d, P265FE_EBITSTREAM, e.what());
-    } catch (const std::bad_alloc&) {
-        return set_err(d, P265FE_ENOMEM, "out of memory");
-    } catch (const std::exception& e) {
-        return set_err(d, P265FE_EBITSTREAM, e.what());
+        cur.hdrs.push_back(std::move(h));
+        cur.slices.push_back(std::move(nal));
     }
 }
 
-int p265fe_picture(p265fe_decoder* d, int i, p265fe_picture_info* out) {
-    if (!d || !out || i < 0 || (size_t)i >= d->jobs.size() || (size_t)i >= d->recs.size()) return P265FE_EINVAL;
-    const PictureJob& j = *d->jobs[i];
-    const PictureRecords& r = d->recs[i];
+// Parse the slice data of the complete pictures on worker threads; append to `out`.
+int parse_pictures(std::vector<std::unique_ptr<PictureJob>>& jobs, p265fe_pictures& out, int n_threads,
+                   std::string& err) {
+    size_t np = jobs.size(), base = out.recs.size();
+    out.recs.resize(base + np);
+    int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(np, 1));
+    std::atomic<size_t> next{0};
+    std::mutex emu;
+    int first_code = 0;
+    size_t first_pic_err = (size_t)-1;
+    auto worker = [&]() {
+        for (;;) {
+            size_t k = next.fetch_add(1);
+            if (k >= np) return;
+            PictureJob& j = *jobs[k];
+            std::vector<SliceRef> sl;
+            for (size_t s = 0; s < j.slices.size(); ++s)
+                sl.push_back(SliceRef{j.hdrs[s].get(), j.slices[s].rbsp.data(), j.slices[s].rbsp.size()});
+            int code = 0;
+            std::string msg;
+            try {
+                decode_picture(*j.act, sl, out.recs[base + k]);
+            } catch (const Unsupported& e) {
+                code = P265FE_EUNSUPPORTED; msg = e.what();
+            } catch (const BitstreamError& e) {
+                code = P265FE_EBITSTREAM; msg = e.what();
+            } catch (const std::bad_alloc&) {
+                code = P265FE_ENOMEM; msg = "out of memory";
+            } catch (const std::exception& e) {
+                code = P265FE_EBITSTREAM; msg = e.what();
+            }
+            if (code) {
+                std::lock_guard<std::mutex> g(emu);
+                if (k < first_pic_err) {
+                    first_pic_err = k;
+                    first_code = code;
+                    err = "picture " + std::to_string(base + k) + ": " + msg;
+                }
+            }
+        }
+    };
+    if (nt <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(worker);
+        for (auto& t : th) t.join();
+    }
+    if (first_code) {
+        out.recs.resize(base);
+        jobs.clear();
+        return first_code;
+    }
+    for (auto& j : jobs) out.jobs.push_back(std::move(j));
+    jobs.clear();
+    return 0;
+}
+
+void fill_info(const PictureJob& j, const PictureRecords& r, p265fe_picture_info* out) {
     const Sps& s = j.act->sps;
     const Pps& p = j.act->pps;
     std::memset(out, 0, sizeof(*out));
@@ -299,10 +282,120 @@ int p265fe_picture(p265fe_decoder* d, int i, p265fe_picture_info* out) {
     out->crop_bottom = (uint16_t)(sh * s.conf_bottom);
     out->nal_unit_type = (uint8_t)j.nal_type;
     out->hash_type = (int8_t)j.hash_type;
-    out->n_slices = (uint16_t)j.nal_idx.size();
+    out->n_slices = (uint16_t)j.slices.size();
     out->n_cus = r.n_cus;
     std::memcpy(out->hash, j.hash, sizeof(out->hash));
+    out->cvs_id = j.cvs;
+    out->max_num_reorder = (uint8_t)s.max_num_reorder;
+    out->output_flag = (uint8_t)(j.output ? 1 : 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t p265fe_abi_version(void) { return P265FE_ABI_VERSION; }
+
+int p265fe_create(p265fe_decoder** out) {
+    if (!out) return P265FE_EINVAL;
+    try {
+        *out = new p265fe_decoder();
+    } catch (...) {
+        return P265FE_ENOMEM;
+    }
     return P265FE_OK;
+}
+
+void p265fe_destroy(p265fe_decoder* d) {
+    if (!d) return;
+    delete d->last;
+    delete d;
+}
+
+const char* p265fe_last_error(p265fe_decoder* d) { return d ? d->err.c_str() : ""; }
+
+int p265fe_feed(p265fe_decoder* d, const uint8_t* data, size_t size, int n_threads, int flags) {
+    if (!d || (!data && size) || (flags & ~P265FE_FLUSH)) return P265FE_EINVAL;
+    d->err.clear();
+    StreamState& st = d->st;
+    try {
+        std::vector<uint8_t> buf;
+        buf.reserve(st.tail.size() + size);
+        buf.insert(buf.end(), st.tail.begin(), st.tail.end());
+        if (size) buf.insert(buf.end(), data, data + size);
+        st.tail.clear();
+        size_t cut = buf.size();
+        if (!(flags & P265FE_FLUSH)) {
+            // the NAL unit after the last start code may continue in the next chunk
+            cut = 0;
+            for (size_t k = buf.size() >= 3 ? buf.size() - 2 : 0; k-- > 0;)
+                if (buf[k] == 0 && buf[k + 1] == 0 && buf[k + 2] == 1) { cut = k; break; }
+            st.tail.assign(buf.begin() + (long)cut, buf.end());
+        }
+        std::vector<Nal> nals = split_nals(buf.data(), cut);
+        for (auto& nal : nals) process_nal(st, std::move(nal));
+        if (flags & P265FE_FLUSH) finish_current(st);
+        int rc = parse_pictures(st.complete, d->ready, n_threads, d->err);
+        if (rc) return rc;
+        return (int)d->ready.jobs.size();
+    } catch (const Unsupported& e) {
+        return set_err(d, P265FE_EUNSUPPORTED, e.what());
+    } catch (const BitstreamError& e) {
+        return set_err(d, P265FE_EBITSTREAM, e.what());
+    } catch (const std::bad_alloc&) {
+        return set_err(d, P265FE_ENOMEM, "out of memory");
+    } catch (const std::exception& e) {
+        return set_err(d, P265FE_EBITSTREAM, e.what());
+    }
+}
+
+int p265fe_take(p265fe_decoder* d, p265fe_pictures** out) {
+    if (!d || !out) return P265FE_EINVAL;
+    *out = nullptr;
+    auto* set = new (std::nothrow) p265fe_pictures();
+    if (!set) return P265FE_ENOMEM;
+    set->jobs = std::move(d->ready.jobs);
+    set->recs = std::move(d->ready.recs);
+    d->ready.jobs.clear();
+    d->ready.recs.clear();
+    *out = set;
+    return (int)set->jobs.size();
+}
+
+int p265fe_pictures_get(const p265fe_pictures* set, int i, p265fe_picture_info* out) {
+    if (!set || !out || i < 0 || (size_t)i >= set->jobs.size()) return P265FE_EINVAL;
+    fill_info(*set->jobs[i], set->recs[i], out);
+    return P265FE_OK;
+}
+
+void p265fe_pictures_free(p265fe_pictures* set) { delete set; }
+
+int p265fe_decode(p265fe_decoder* d, const uint8_t* data, size_t size, int n_threads) {
+    if (!d || (!data && size)) return P265FE_EINVAL;
+    d->st = StreamState();
+    d->ready = p265fe_pictures();
+    delete d->last;
+    d->last = nullptr;
+    int n = p265fe_feed(d, data, size, n_threads, P265FE_FLUSH);
+    if (n < 0) return n;
+    p265fe_pictures* set = nullptr;
+    int rc = p265fe_take(d, &set);
+    if (rc < 0) return rc;
+    // output order of the whole stream: by (coded video sequence, POC) among output pictures
+    std::vector<PictureJob*> outv;
+    for (auto& j : set->jobs)
+        if (j->output) outv.push_back(j.get());
+    std::stable_sort(outv.begin(), outv.end(), [](const PictureJob* a, const PictureJob* b) {
+        return a->cvs != b->cvs ? a->cvs < b->cvs : a->poc < b->poc;
+    });
+    for (size_t r = 0; r < outv.size(); ++r) outv[r]->output_rank = (int)r;
+    d->last = set;
+    return (int)set->jobs.size();
+}
+
+int p265fe_picture(p265fe_decoder* d, int i, p265fe_picture_info* out) {
+    if (!d || !d->last) return P265FE_EINVAL;
+    return p265fe_pictures_get(d->last, i, out);
 }
 
 }  // extern "C"

@@ -220,8 +220,11 @@ Sps parse_sps(BitReader& br) {
     if (s.log2_max_poc_lsb > 16) bs_fail("log2_max_pic_order_cnt_lsb_minus4 > 12");
     int ordering = br.flag();
     for (int i = ordering ? 0 : s.max_sub_layers_minus1; i <= s.max_sub_layers_minus1; ++i) {
-        br.ue(); br.ue(); br.ue();
+        br.ue();                                       // sps_max_dec_pic_buffering_minus1
+        s.max_num_reorder = (int)br.ue();              // sps_max_num_reorder_pics (HighestTid = last)
+        br.ue();                                       // sps_max_latency_increase_plus1
     }
+    if (s.max_num_reorder > 16) bs_fail("sps_max_num_reorder_pics > 16");
     s.log2_min_cb = 3 + (int)br.ue();
     s.log2_ctb = s.log2_min_cb + (int)br.ue();
     s.log2_min_tb = 2 + (int)br.ue();

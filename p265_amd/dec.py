@@ -5,7 +5,8 @@
 ``-b/--bitstream`` and ``-o/--output`` keep the reference's meaning (its ``-o`` is
 declared but never written, p265:9); ``--skip-syntax-dump`` is accepted for command
 line compatibility (this decoder writes no syntax logs).  Parsing runs on host threads
-(libp265fe.so), reconstruction on the MI355X (libp265r.so).
+(libp265fe.so), reconstruction on the MI355X (libp265r.so); the file is streamed
+(bounded memory) and the YUV written in output order as pictures complete.
 """
 import argparse
 import sys
@@ -28,17 +29,13 @@ def parse_cmd(argv=None):
 
 def main(argv=None):
     a = parse_cmd(argv)
-    data = open(a.bitstream, "rb").read()
     t0 = time.time()
-    frames = decoder.decode_bytes(data, device=a.device, batch=a.batch, threads=a.threads,
-                                  verify_hash=not a.no_verify)
+    st = decoder.decode_file(a.bitstream, a.output, device=a.device, batch=a.batch, threads=a.threads,
+                             verify_hash=not a.no_verify)
     dt = time.time() - t0
-    if a.output:
-        decoder.write_yuv(frames, a.output)
-    checked = sum(1 for f in frames if f.hash_ok is not None)
-    bad = sum(1 for f in frames if f.hash_ok is False)
-    print("decoded %d pictures in %.3f s; picture hash SEI checked %d, mismatched %d" % (len(frames), dt, checked, bad))
-    return 1 if bad else 0
+    print("decoded %d pictures in %.3f s; picture hash SEI checked %d, mismatched %d"
+          % (st["pictures"], dt, st["hash_checked"], st["hash_mismatch"]))
+    return 1 if st["hash_mismatch"] else 0
 
 
 if __name__ == "__main__":

@@ -4,16 +4,23 @@ This is the call stack the reference's ``p265 -b stream.bin -o out.yuv`` (p265:7
 dec.py:6-64) would have if its reconstruction worked: parsing runs in
 the native front-end (libp265fe.so, host threads), reconstruction + deblocking + SAO
 run in the HIP back-end (libp265r.so) in batches of pictures, and the decoded
-pictures come back in output (POC) order, cropped to the conformance window
-(sps.py:48-53; the reference parses it but never uses it), and checked against the
-stream's decoded-picture-hash SEI when present (D.3.19).
+pictures come back in output order, cropped to the conformance window (sps.py:48-53;
+the reference parses it but never uses it), and checked against the stream's
+decoded-picture-hash SEI when present (D.3.19).
+
+Streaming: ``decode_chunks`` feeds the parser chunk by chunk on a background thread
+(the ctypes calls release the GIL), so parsing overlaps the GPU batches and memory
+stays bounded by a few chunks plus one batch; output order follows the bumping
+process of C.5.2.2 (``OutputQueue``).  ``decode_file`` streams a file to YUV.
 
 No CPU reconstruction exists on this path: a missing library or GPU raises.
 """
 import os
+import queue
+import threading
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Iterable, Iterator, List, Optional
 
 import numpy as np
 
@@ -44,54 +51,164 @@ class HashMismatch(RuntimeError):
     pass
 
 
-def _batches(items, key, size):
-    cur, k0 = [], None
-    for it in items:
-        k = key(it)
-        if cur and (k != k0 or len(cur) >= size):
-            yield cur
-            cur = []
-        cur.append(it)
-        k0 = k
-    if cur:
-        yield cur
+class OutputQueue:
+    """Output order: the "bumping" process of C.5.2.2 without the DPB-fullness trigger.
+
+    Inside a coded video sequence a picture leaves, smallest POC first, as soon as more
+    than sps_max_num_reorder_pics pictures wait; a new coded video sequence (IRAP with
+    NoRaslOutputFlag) or the end of the stream outputs everything waiting."""
+
+    def __init__(self):
+        self.waiting = []
+        self.cvs = None
+
+    def push(self, item, cvs, poc, max_num_reorder, output_flag):
+        out = []
+        if self.cvs is not None and cvs != self.cvs:
+            out += self.flush()
+        self.cvs = cvs
+        if output_flag:
+            self.waiting.append((poc, item))
+        while len(self.waiting) > max_num_reorder:
+            k = min(range(len(self.waiting)), key=lambda i: self.waiting[i][0])
+            out.append(self.waiting.pop(k)[1])
+        return out
+
+    def flush(self):
+        out = [it for _, it in sorted(self.waiting, key=lambda e: e[0])]
+        self.waiting = []
+        return out
 
 
-def decode_bytes(data: bytes, device: int = 0, batch: int = 64, threads: int = 0,
-                 verify_hash: bool = True) -> List[DecodedFrame]:
-    """Decode a whole stream; returns the output pictures in output order.
+def _chunks(data, size):
+    for i in range(0, len(data), size):
+        yield data[i:i + size]
 
-    Picture hashes are computed on host threads (the C hash releases the GIL) while the
-    next batch decodes on the GPU."""
-    pics = bitstream.decode_stream(data, threads=threads)
-    frames = []
+
+def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 64, threads: int = 0,
+                  verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4) -> Iterator[DecodedFrame]:
+    """Decode a stream given as an iterable of byte chunks; yields frames in output order.
+
+    A GPU batch runs when ``batch`` pictures are pending, when the parameter set changes,
+    or -- if the parser has nothing else ready -- when ``min_batch`` are pending."""
+    parser = bitstream.StreamParser(threads=threads)
+    q = queue.Queue(maxsize=max(1, prefetch))
+    stop = threading.Event()
+
+    def produce():
+        try:
+            for ch in chunks:
+                if stop.is_set():
+                    return
+                pics = parser.feed(ch)
+                if pics:
+                    q.put(pics)
+            q.put(parser.feed(b"", flush=True))
+            q.put(None)
+        except BaseException as e:  # noqa: BLE001 -- handed to the consumer
+            q.put(e)
+
+    th = threading.Thread(target=produce, name="p265fe-parse", daemon=True)
+    th.start()
     contexts = {}
     pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
-    checks = []
-    try:
-        for group in _batches(list(enumerate(pics)), lambda it: it[1].params.tobytes(), batch):
-            key = group[0][1].params.tobytes()
-            ctx = contexts.get(key)
-            if ctx is None:
-                ctx = contexts[key] = recon.ReconContext(group[0][1].params, device=device)
-            outs = ctx.decode([d.picture for _, d in group])
-            for (i, d), planes in zip(group, outs):
-                fr = DecodedFrame(poc=d.poc, output_rank=d.output_rank, decode_index=i,
-                                  planes=planes, crop=tuple(int(v) for v in d.crop), hash_ok=None)
-                if d.hash is not None:
-                    checks.append((fr, d, [pool.submit(bitstream.plane_hash, planes[c], d.hash_type) for c in range(3)]))
-                if d.output_rank >= 0:
-                    frames.append(fr)
-        for fr, d, futs in checks:
+    outq = OutputQueue()
+    rank = 0
+
+    def run(group):
+        key = group[0].params.tobytes()
+        ctx = contexts.get(key)
+        if ctx is None:
+            ctx = contexts[key] = recon.ReconContext(group[0].params, device=device)
+        outs = ctx.decode([d.picture for d in group])
+        ready = []
+        for d, planes in zip(group, outs):
+            fr = DecodedFrame(poc=d.poc, output_rank=-1, decode_index=int(d.picture.meta["decode_index"]),
+                              planes=planes, crop=tuple(int(v) for v in d.crop), hash_ok=None)
+            futs = None
+            if d.hash is not None:
+                futs = [pool.submit(bitstream.plane_hash, planes[c], d.hash_type) for c in range(3)]
+            ready += outq.push((fr, d, futs), d.cvs_id, d.poc, d.max_num_reorder, d.output_flag)
+        return ready
+
+    def emit(item):
+        nonlocal rank
+        fr, d, futs = item
+        if futs is not None:
             fr.hash_ok = all(f.result() == d.hash[c] for c, f in enumerate(futs))
             if verify_hash and not fr.hash_ok:
-                raise HashMismatch("picture %d (POC %d): decoded picture hash SEI mismatch" % (fr.decode_index, d.poc))
+                raise HashMismatch("picture %d (POC %d): decoded picture hash SEI mismatch" % (fr.decode_index, fr.poc))
+        fr.output_rank = rank
+        rank += 1
+        return fr
+
+    try:
+        pending = []
+        while True:
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            end = item is None
+            for d in item or []:
+                if pending and (len(pending) >= batch or d.params.tobytes() != pending[0].params.tobytes()):
+                    for it in run(pending):
+                        yield emit(it)
+                    pending = []
+                pending.append(d)
+            # the parser has nothing ready right now: decode what is pending instead of waiting
+            if pending and (end or (q.empty() and len(pending) >= min_batch)):
+                for it in run(pending):
+                    yield emit(it)
+                pending = []
+            if end:
+                break
+        for it in outq.flush():
+            yield emit(it)
     finally:
+        stop.set()
+        while th.is_alive():
+            try:
+                q.get(timeout=0.05)
+            except queue.Empty:
+                pass
         pool.shutdown(wait=True)
         for ctx in contexts.values():
             ctx.close()
-    frames.sort(key=lambda f: f.output_rank)
-    return frames
+
+
+def decode_bytes(data: bytes, device: int = 0, batch: int = 64, threads: int = 0,
+                 verify_hash: bool = True, chunk: int = 1 << 20) -> List[DecodedFrame]:
+    """Decode a whole stream held in memory; returns the output pictures in output order."""
+    return list(decode_chunks(_chunks(data, chunk), device=device, batch=batch, threads=threads,
+                              verify_hash=verify_hash))
+
+
+def _file_chunks(path, chunk):
+    with open(path, "rb") as f:
+        while True:
+            b = f.read(chunk)
+            if not b:
+                return
+            yield b
+
+
+def decode_file(path: str, output: Optional[str] = None, chunk: int = 8 << 20, **kw) -> dict:
+    """Stream a bitstream file to a cropped I420 YUV file in output order; returns counts."""
+    n = checked = bad = 0
+    f = open(output, "wb") if output else None
+    try:
+        for fr in decode_chunks(_file_chunks(path, chunk), **kw):
+            n += 1
+            if fr.hash_ok is not None:
+                checked += 1
+                bad += int(not fr.hash_ok)
+            if f:
+                for p in fr.cropped():
+                    f.write(np.ascontiguousarray(p).tobytes())
+    finally:
+        if f:
+            f.close()
+    return {"pictures": n, "hash_checked": checked, "hash_mismatch": bad}
 
 
 def write_yuv(frames: List[DecodedFrame], path: str):

@@ -261,7 +261,7 @@ DEFAULTS = dict(
     slice_chroma_offsets=None,  # (cb, cr) per independent slice, or None
     deblocking="on",            # "on" | "off" (pps disabled) | "override" (random per slice)
     lf_across_slices=1, lf_across_tiles=1, conf_window=None, hash_sei=None,   # hash_sei: None | "md5" | "crc" | "checksum"
-    frames=1, idr_period=0, log2_max_poc_lsb=8,
+    frames=1, idr_period=0, log2_max_poc_lsb=8, poc_order=None, max_reorder=0,   # poc_order: POC per frame (IDR first)
     split_prob=0.55, tf_split_prob=0.5, nxn_prob=0.4, cbf_prob=0.7, chroma_cbf_prob=0.35, pcm_prob=0.08,
     bypass_prob=0.1, tskip_prob=0.3, density=0.25, big_prob=0.03,
 )
@@ -352,7 +352,7 @@ class StreamGen:
             bw.u(0, 1)
         bw.ue(0); bw.ue(0)                               # bit depths 8
         bw.ue(c["log2_max_poc_lsb"] - 4)
-        bw.u(1, 1); bw.ue(1); bw.ue(0); bw.ue(0)
+        bw.u(1, 1); bw.ue(1 + c["max_reorder"]); bw.ue(c["max_reorder"]); bw.ue(0)
         bw.ue(c["min_cb_log2"] - 3); bw.ue(c["ctb_log2"] - c["min_cb_log2"])
         bw.ue(c["min_tb_log2"] - 2); bw.ue(c["max_tb_log2"] - c["min_tb_log2"])
         bw.ue(c["max_th_depth"]); bw.ue(c["max_th_depth"])
@@ -435,7 +435,9 @@ class StreamGen:
         max_lsb = 1 << c["log2_max_poc_lsb"]
         for f in range(c["frames"]):
             idr = f == 0 or (c["idr_period"] and f % c["idr_period"] == 0)
-            if idr:
+            if c["poc_order"] is not None:
+                idr, poc = f == 0, c["poc_order"][f]
+            elif idr:
                 poc = 0
             nal_type = 19 if idr else 1
             nals, pic = self.picture(nal_type, poc % max_lsb)

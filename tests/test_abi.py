@@ -82,13 +82,13 @@ def test_front_end_exports_every_declared_symbol():
     from p265_amd import bitstream
     lib = bitstream.load()
     names = sorted(set(re.findall(r"\b(p265fe_[a-z_]+)\s*\(", open(FE_HEADER).read())))
-    assert len(names) >= 7
+    assert len(names) >= 11
     for n in names:
         assert hasattr(lib, n), n
         assert n in bitstream.SIGNATURES, n
-    assert lib.p265fe_abi_version() == 1
+    assert lib.p265fe_abi_version() == 2
     # p265fe_picture_info layout: 32 B params + pointers/counters + 48 B hash
-    assert ctypes.sizeof(bitstream.PictureInfoC) == 152
+    assert ctypes.sizeof(bitstream.PictureInfoC) == 160
     h = ctypes.c_void_p()
     assert lib.p265fe_create(ctypes.byref(h)) == 0
     assert lib.p265fe_picture(h, 0, None) == bitstream.EINVAL

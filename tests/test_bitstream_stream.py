@@ -1,0 +1,124 @@
+"""Streaming parse (p265fe_feed / StreamParser) and output ordering, CPU only.
+
+Feeding a stream in chunks of any size must give exactly the pictures (records and
+metadata) of the one-shot parse: parameter sets, POC state, partial access units and
+partial NAL units carry over between p265fe_feed calls.  Output order follows the
+bumping process of C.5.2.2 (decoder.OutputQueue) and agrees with the one-shot output
+ranks, also for a stream whose pictures are reordered (sps_max_num_reorder_pics = 1).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import streamgen
+from p265_amd import bitstream
+from p265_amd.decoder import OutputQueue
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _sanity():
+    return open(os.path.join(GOLDEN, "sanity.bin"), "rb").read()
+
+
+STREAMS = {
+    "sanity": _sanity,
+    "tiles_wpp_slices_md5": lambda: streamgen.StreamGen(
+        21, tiles=(2, 2), wpp=True, slices=[(0, False), (9, True), (30, False)], hash_sei="md5", frames=3)
+    .stream()[0],
+    "pcm_bypass_qp_crc": lambda: streamgen.StreamGen(
+        22, pcm=(3, 4, True), bypass=True, qp_delta_depth=1, hash_sei="crc", frames=2).stream()[0],
+    "reorder": lambda: streamgen.StreamGen(23, frames=6, poc_order=[0, 2, 1, 4, 3, 5], max_reorder=1).stream()[0],
+    "idr_period": lambda: streamgen.StreamGen(24, frames=5, idr_period=2).stream()[0],
+}
+
+
+def _same(a, b):
+    assert a.params.tobytes() == b.params.tobytes()
+    assert (a.poc, a.cvs_id, a.nal_unit_type, a.n_slices, a.n_cus, a.hash_type, a.hash, a.crop,
+            a.max_num_reorder, a.output_flag) == \
+           (b.poc, b.cvs_id, b.nal_unit_type, b.n_slices, b.n_cus, b.hash_type, b.hash, b.crop,
+            b.max_num_reorder, b.output_flag)
+    assert a.picture.meta["decode_index"] == b.picture.meta["decode_index"]
+    for f in ("ctus", "tbs", "coef"):
+        assert np.array_equal(getattr(a.picture, f), getattr(b.picture, f))
+    if b.picture.nofilter is None:
+        assert a.picture.nofilter is None
+    else:
+        assert np.array_equal(a.picture.nofilter, b.picture.nofilter)
+
+
+def _feed_all(data, sizes, threads=2):
+    p = bitstream.StreamParser(threads=threads)
+    out, pos, i = [], 0, 0
+    while pos < len(data):
+        n = sizes[i % len(sizes)]
+        out += p.feed(data[pos:pos + n])
+        pos += n
+        i += 1
+    out += p.feed(b"", flush=True)
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(STREAMS))
+@pytest.mark.parametrize("sizes", [[1 << 30], [4096], [997], [1, 2, 3, 5, 8, 13, 21, 34, 55, 89, 144, 233, 377, 610]],
+                         ids=["whole", "4096", "997", "fib"])
+def test_chunked_feed_equals_whole_stream(name, sizes):
+    data = STREAMS[name]()
+    whole = bitstream.decode_stream(data)
+    got = _feed_all(data, sizes)
+    assert len(got) == len(whole) > 0
+    for a, b in zip(got, whole):
+        _same(a, b)
+        assert a.output_rank == -1
+
+
+def test_random_chunk_boundaries():
+    data = STREAMS["tiles_wpp_slices_md5"]()
+    whole = bitstream.decode_stream(data)
+    rng = random.Random(265)
+    for _ in range(12):
+        sizes = [rng.randint(1, 3000) for _ in range(50)]
+        got = _feed_all(data, sizes, threads=rng.choice([1, 3]))
+        assert len(got) == len(whole)
+        for a, b in zip(got, whole):
+            _same(a, b)
+
+
+def _output_pocs(pics):
+    q, out = OutputQueue(), []
+    for d in pics:
+        out += q.push(d, d.cvs_id, d.poc, d.max_num_reorder, d.output_flag)
+    return [d.poc for d in out + q.flush()]
+
+
+def test_output_queue_reorders_by_poc():
+    data = STREAMS["reorder"]()
+    pics = _feed_all(data, [777])
+    assert [p.poc for p in pics] == [0, 2, 1, 4, 3, 5]
+    assert all(p.max_num_reorder == 1 for p in pics)
+    assert _output_pocs(pics) == [0, 1, 2, 3, 4, 5]
+    whole = bitstream.decode_stream(data)            # the one-shot ranks agree
+    assert [w.poc for w in sorted(whole, key=lambda w: w.output_rank)] == [0, 1, 2, 3, 4, 5]
+
+
+def test_output_queue_flushes_at_each_coded_video_sequence():
+    pics = _feed_all(STREAMS["idr_period"](), [4096])
+    assert [p.cvs_id for p in pics] == [0, 0, 1, 1, 2]
+    assert _output_pocs(pics) == [0, 1, 0, 1, 0]
+    q = OutputQueue()
+    assert q.push("a", 0, 5, 2, True) == [] and q.push("b", 0, 3, 2, True) == []
+    assert q.push("c", 1, 0, 2, True) == ["b", "a"]              # new sequence: earlier pictures leave
+    assert q.push("d", 1, 1, 0, False) == ["c"]                  # not output itself, bumps "c"
+    assert q.flush() == []
+
+
+def test_streaming_errors():
+    data = STREAMS["sanity"]()
+    p = bitstream.StreamParser()
+    assert p.feed(data[:5000]) == []                             # parameter sets + part of picture 0
+    with pytest.raises(bitstream.BitstreamError):
+        p.feed(data[5000:9000], flush=True)                      # picture 0 ends truncated
+    assert bitstream.StreamParser().feed(b"\x00\x00", flush=True) == []

@@ -43,6 +43,28 @@ int main(int argc, char** argv) {
                 ++err;
             }
             p265fe_destroy(dec);
+            // the same bytes fed in random chunks: same picture count as the one-shot parse
+            p265fe_decoder* sd = nullptr;
+            p265fe_create(&sd);
+            size_t pos = 0;
+            int rs = 0;
+            while (pos < d.size() && rs >= 0) {
+                size_t n = 1 + rng() % 4096;
+                if (n > d.size() - pos) n = d.size() - pos;
+                rs = p265fe_feed(sd, d.data() + pos, n, 1 + (it & 1), 0);
+                pos += n;
+            }
+            if (rs >= 0) rs = p265fe_feed(sd, nullptr, 0, 1, P265FE_FLUSH);
+            p265fe_pictures* set = nullptr;
+            int ns = p265fe_take(sd, &set);
+            if (rs >= 0 && r >= 0 && ns != r) {
+                std::fprintf(stderr, "chunked feed gave %d pictures, one-shot %d\n", ns, r);
+                return 1;
+            }
+            p265fe_picture_info info2;
+            for (int i = 0; i < ns; ++i) p265fe_pictures_get(set, i, &info2);
+            p265fe_pictures_free(set);
+            p265fe_destroy(sd);
         }
     }
     std::printf("fuzz done: %d decoded, %d rejected\n", ok, err);
