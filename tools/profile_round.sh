@@ -7,7 +7,7 @@ TAG=${1:-r1}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python bench.py --steps 3 --warmup 1 --frames 512 --unique 2 --no-cpu-baseline"
+B="python bench.py --steps 3 --warmup 1 --frames 512 --unique 2 --no-cpu-baseline --no-e2e"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- $B > $OUT/kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fe -- $B > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o wr -- $B > $OUT/write.log 2>&1
