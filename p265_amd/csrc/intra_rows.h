@@ -70,12 +70,12 @@ __device__ __forceinline__ void* lds_ptr(uint32_t a) {
     return (void*)(__attribute__((address_space(3))) void*)(uintptr_t)a;
 }
 
-struct WaveLds {                 // one wave's private CTU state (6816 B)
+struct WaveLds {                 // one wave's private CTU state (6544 B)
     uint8_t  y[64 * 64];         // interior luma, stride 64
     uint8_t  c[2][32 * 32];      // interior chroma, stride 32
     uint8_t  yleft[64];          // right column of the previous CTU of this row
     uint8_t  cleft[2][32];
-    uint16_t ref[2][136];        // raw / final linear reference arrays
+    uint8_t  ref[2][136];        // raw / final linear reference arrays (8-bit samples)
 };
 
 struct RowCtrl {                 // 256 B at the start of dynamic LDS
@@ -168,8 +168,8 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
     } else {
         // ---- gather (+ substitution) --------------------------------------------------
         const int filt = PAIR ? 0 : (int)((w0 >> 24) & 3u);
-        uint16_t* const R0 = PAIR ? L.ref[half] : L.ref[0];
-        uint16_t* const RF = (PAIR || !filt) ? R0 : L.ref[1];
+        uint8_t* const R0 = PAIR ? L.ref[half] : L.ref[0];
+        uint8_t* const RF = (PAIR || !filt) ? R0 : L.ref[1];
         // sources: left column (entries 0..2n-1), corner (2n), top row (2n+1..4n)
         const uint8_t* const lbase = xr == 0 ? lcol : org - 1;
         const int lstep = xr == 0 ? 1 : ist;
@@ -198,7 +198,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                 }
                 const uint8_t* src = s < 2 * n ? lbase + (2 * n - 1 - s) * lstep : (s == 2 * n ? cptr : tbase + (s - 2 * n - 1));
                 const int v = none ? 128 : (int)*src;
-                R0[k] = (uint16_t)v;
+                R0[k] = (uint8_t)v;
                 if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) dcs += v;
             }
         }
@@ -225,12 +225,12 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                             f = ((int)R0[k - 1] + 2 * f + (int)R0[k + 1] + 2) >> 2;
                         }
                     }
-                    RF[k] = (uint16_t)f;
+                    RF[k] = (uint8_t)f;
                 }
             }
             wave_sync();
         }
-        const uint16_t* const R = RF;
+        const uint8_t* const R = RF;
         // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------
         if (mode == 0) {
             const int trs = R[3 * n + 1], bls = R[n - 1];

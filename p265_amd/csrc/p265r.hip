@@ -224,6 +224,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
 int launch_rows(p265r_ctx* ctx, p265r_batch* b) {
     switch (ctx->row_waves) {
         case 4: return launch_rows_w<4>(ctx, b);
+        case 6: return launch_rows_w<6>(ctx, b);
+        case 10: return launch_rows_w<10>(ctx, b);
         case 16: return launch_rows_w<16>(ctx, b);
         default: return launch_rows_w<8>(ctx, b);
     }
@@ -292,7 +294,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
-        if (w == 4 || w == 8 || w == 16) ctx->row_waves = w;
+        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 16) ctx->row_waves = w;
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
