@@ -167,8 +167,13 @@ int  p265r_submit(p265r_ctx* ctx, const p265r_picture* pics, int n_pics);
 /* ... then block until outputs are written into the pictures given to submit. */
 int  p265r_wait(p265r_ctx* ctx);
 
-/* Block until the context stream is idle. */
+/* Block until the context's streams are idle. */
 int  p265r_sync(p265r_ctx* ctx);
+/* Batch pipelining (no counterpart in the reference; a throughput knob of this back-end):
+ * batches uploaded afterwards are bound round-robin to `depth` (1..4) HIP streams, so the
+ * residual and loop-filter phases of one batch run beside the intra phase of another.
+ * Runs of one batch stay ordered; p265r_sync waits for every stream.  Default 1. */
+int  p265r_set_pipeline(p265r_ctx* ctx, int depth);
 /* Enable (1, which also starts a new accumulation) / disable (0) per-phase HIP-event
  * timing of every p265r_batch_run; read the last run's timings, or the sums over all runs
  * since enabling (runs may be queued back to back: nothing here waits per run). */

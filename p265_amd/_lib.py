@@ -72,6 +72,7 @@ SIGNATURES = {
     "p265r_submit": (ctypes.c_int, [_vp, ctypes.POINTER(PictureC), ctypes.c_int]),
     "p265r_wait": (ctypes.c_int, [_vp]),
     "p265r_sync": (ctypes.c_int, [_vp]),
+    "p265r_set_pipeline": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265r_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265r_last_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
     "p265r_timings_total": (ctypes.c_int, [_vp, ctypes.POINTER(Timings), ctypes.POINTER(ctypes.c_int)]),

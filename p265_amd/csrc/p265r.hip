@@ -97,6 +97,12 @@ struct p265r_ctx {
     bool stage_pinned = false;
     void* cache_mem = nullptr;
     size_t cache_bytes = 0;
+    // batch pipelining (p265r_set_pipeline): batches are bound round-robin to `pipeline`
+    // streams (lane 0 = stream), so one batch's residual / loop-filter phases run beside
+    // another batch's intra kernel
+    int pipeline = 1;
+    int next_lane = 0;
+    std::vector<hipStream_t> lanes;   // lanes[0] == stream
 };
 
 struct p265r_batch {
@@ -110,6 +116,7 @@ struct p265r_batch {
     ResJob* d_jobs[RC_NUM] = {};
     int n_jobs[RC_NUM] = {};
     std::vector<DevPic> h_pics;
+    hipStream_t stream = nullptr;  // the context lane this batch runs on
     bool sao = false;
     bool dbk = false;          // some CTU of the batch has deblocking on
     bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
@@ -199,11 +206,11 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
         std::memset(dbg, 0, sizeof(int) * grid * W * 3);
         fprintf(stderr, "[p265r] rows kernel W=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, grid, lds, fs, per_cu);
     }
-    fn<<<grid, 64 * W, lds, ctx->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
+    fn<<<grid, 64 * W, lds, b->stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
     HIP_TRY(hipGetLastError());
     if (dbg) {
         for (int it = 0; it < 100; ++it) {
-            if (hipStreamQuery(ctx->stream) == hipSuccess) break;
+            if (hipStreamQuery(b->stream) == hipSuccess) break;
             struct timespec ts{0, 100000000};
             nanosleep(&ts, nullptr);
             if (it == 99) {
@@ -299,6 +306,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) ctx->lanes.push_back(ctx->stream);
     if (e == hipSuccess) {
         int8_t ang[35];
         int16_t inv[35];
@@ -318,9 +326,11 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
 void p265r_destroy(p265r_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->pending) { (void)hipStreamSynchronize(ctx->stream); p265r_batch_free(ctx, ctx->pending); }
+    for (hipStream_t st : ctx->lanes) (void)hipStreamSynchronize(st);
+    if (ctx->pending) p265r_batch_free(ctx, ctx->pending);
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
     for (auto& e : ctx->spare) (void)hipEventDestroy(e);
+    for (size_t i = 1; i < ctx->lanes.size(); ++i) (void)hipStreamDestroy(ctx->lanes[i]);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
     if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
@@ -440,6 +450,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         b->bytes = total;
     }
     b->n_pics = n_pics;
+    b->stream = ctx->stream;
+    if (ctx->pipeline > 1) b->stream = ctx->lanes[ctx->next_lane++ % ctx->pipeline];
     b->sao = sao;
     b->dbk = dbk;
     b->recon_input = recon_input;
@@ -561,7 +573,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
 int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
+    hipStream_t s = b->stream;
     const Geo& g = ctx->geo;
     p265r_timings tm{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -670,12 +682,12 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
         for (int c = 0; c < 3; ++c) {
             if (pics[i].out[c])
                 HIP_TRY(hipMemcpy2DAsync(pics[i].out[c], wd[c], b->h_pics[i].out[c], g.stride[c], wd[c], ht[c],
-                                         hipMemcpyDeviceToHost, ctx->stream));
+                                         hipMemcpyDeviceToHost, b->stream));
             if (pics[i].recon[c] && !b->recon_input)
                 HIP_TRY(hipMemcpy2DAsync(pics[i].recon[c], wd[c], b->h_pics[i].rec[c], g.stride[c], wd[c], ht[c],
-                                         hipMemcpyDeviceToHost, ctx->stream));
+                                         hipMemcpyDeviceToHost, b->stream));
         }
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
     int err = 0;
     HIP_TRY(hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
@@ -690,6 +702,7 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     (void)hipSetDevice(ctx->device);
     if (ctx->pending == b) ctx->pending = nullptr;
     hipError_t e = hipSuccess;
+    if (b->stream && b->stream != ctx->stream) e = hipStreamSynchronize(b->stream);   // its lane may still run it
     if (b->mem) {
         // keep the larger of (cache, this allocation) for the next upload; callers free a batch
         // only once its work is complete (download/sync), and reuse is ordered on ctx->stream
@@ -732,7 +745,20 @@ int p265r_wait(p265r_ctx* ctx) {
 int p265r_sync(p265r_ctx* ctx) {
     if (!ctx) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (hipStream_t st : ctx->lanes) HIP_TRY(hipStreamSynchronize(st));
+    return P265R_OK;
+}
+
+int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
+    if (!ctx || depth < 1 || depth > 4) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    while ((int)ctx->lanes.size() < depth) {
+        hipStream_t st = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        ctx->lanes.push_back(st);
+    }
+    ctx->pipeline = depth;
+    ctx->next_lane = 0;
     return P265R_OK;
 }
 

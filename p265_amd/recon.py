@@ -143,6 +143,10 @@ class ReconContext:
     def sync(self):
         _lib.check(self.lib.p265r_sync(self.handle), "p265r_sync")
 
+    def set_pipeline(self, depth):
+        """Bind batches uploaded from now on round-robin to `depth` streams (p265r_set_pipeline)."""
+        _lib.check(self.lib.p265r_set_pipeline(self.handle, int(depth)), "p265r_set_pipeline")
+
     def set_timing(self, on=True):
         _lib.check(self.lib.p265r_set_timing(self.handle, int(bool(on))), "p265r_set_timing")
 

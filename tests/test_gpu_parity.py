@@ -141,6 +141,29 @@ def test_resident_batch_rerun_is_stable(recon_mod):
             np.testing.assert_array_equal(first[i][c], second[i][c])
 
 
+def test_pipelined_batches(recon_mod):
+    """p265r_set_pipeline: three resident batches on different streams, each run several times
+    back to back with the runs interleaved across streams, every output equals the oracle."""
+    params = R.make_params(pic_width=320, pic_height=192)
+    sets = [[synth.make_picture(params, 700 + 10 * k + s, perf=bool(s % 2)) for s in range(3)] for k in range(3)]
+    pd = R.params_dict(params)
+    with recon_mod.ReconContext(params) as ctx:
+        ctx.set_pipeline(2)
+        bs = [ctx.upload(p) for p in sets]
+        for _ in range(3):
+            for b in bs:
+                ctx.run(b)
+        ctx.sync()
+        outs = [ctx.download(b) for b in bs]
+        for b in bs:
+            b.free()
+    for k, pics in enumerate(sets):
+        for i, p in enumerate(pics):
+            ref = O.decode_picture(pd, p.as_oracle_dict())[1]
+            for c in range(3):
+                np.testing.assert_array_equal(outs[k][i][c], ref[c], err_msg="set %d pic %d c%d" % (k, i, c))
+
+
 def test_invalid_records_rejected(recon_mod):
     params = R.make_params(pic_width=64, pic_height=64)
     pic = synth.make_picture(params, 3)
