@@ -39,6 +39,8 @@ struct DevPic {                 // per picture, device-resident table
     IntraJob* jobs;             // same index space as tbs (jobs of a CTU start at tb_begin)
     uint32_t* jcount;           // per CTU: luma jobs | chroma jobs << 16 (luma listed first)
     uint8_t* dbk_map;           // per 8x8 luma block (loopfilter.h), nullptr without deblocking
+    int32_t  pool_rel;          // residual pool element index of coefficient pool element 0 (<= 0)
+    uint32_t zero_off;          // residual pool element index of a 256-sample zero block
 };
 
 struct Geo {                    // batch-uniform geometry

@@ -31,7 +31,9 @@ namespace p265r {
 //  w1: [0,8) intraPredAngle (int8)  [8,21) -invAngle  21 availability bit 32
 //  w2: availability bits 0..31 (unit u: k in [u*us, u*us+us) for u < L, corner u = L,
 //      top units u > L; us = 4 luma / 2 chroma samples, L = 2N/us)
-//  w3, w4: residual element offset of half 0 (luma / Cb) and half 1 (Cr)
+//  w3, w4: residual element offset of half 0 (luma / Cb) and half 1 (Cr), int32 relative to
+//      the residual pool for every kind of TB: bypass/PCM samples at a negative offset into
+//      the coefficient pool (DevPic::pool_rel), uncoded halves at a zero block (zero_off)
 //  w5: fast-path job (intra_rows.h recon_fast*): bit 31 set for luma 4x4 .. 16x16 and Cb+Cr
 //      4x4 pairs, not PCM, whose available reference samples form ONE contiguous run
 //      [fa, la] of the linear order (or none): substitution (8.4.4.2.2) is then
@@ -116,9 +118,13 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const uint32_t f1 = pair ? next.flags : 0u;
             // half 0 = luma / Cb, half 1 = Cr (an unpaired Cr TB lives in half 1)
             const uint32_t fh0 = cm == 2 ? 0u : f0, fh1 = cm == 2 ? f0 : f1;
-            const uint32_t off0 = cm == 2 ? 0u : rec.coef_off, off1 = cm == 2 ? rec.coef_off : (pair ? next.coef_off : 0u);
             auto raw = [](uint32_t f) { return (f & (P265R_TB_BYPASS | P265R_TB_PCM)) ? 1u : 0u; };
             auto coded = [](uint32_t f) { return (f & (P265R_TB_CBF | P265R_TB_PCM)) ? 1u : 0u; };
+            auto roff = [&](uint32_t f, uint32_t off) {
+                return !coded(f) ? P.zero_off : (raw(f) ? off + (uint32_t)P.pool_rel : off);
+            };
+            const uint32_t off0 = cm == 2 ? P.zero_off : roff(f0, rec.coef_off);
+            const uint32_t off1 = cm == 2 ? roff(f0, rec.coef_off) : (pair ? roff(f1, next.coef_off) : P.zero_off);
             IntraJob J;
             J.w[0] = ofs | (uint32_t)(lg - 2) << 13 | cm << 15 | (uint32_t)mode << 17 |
                      ((f0 & P265R_TB_PCM) ? J_PCM : 0u) | filt << 24 | raw(fh0) << 26 | raw(fh1) << 27 |

@@ -632,19 +632,13 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const int ls = 2 * lg - (pr ? 5 : 6);
                 const int S = ls > 0 ? (1 << ls) : 1;
                 const int sidx = hl * S < (1 << (2 * lg)) ? hl * S : 0;
-                const int16_t* base = ((w0 >> (26 + h)) & 1u) ? pool : resid;
-                return reinterpret_cast<const uint4*>(base + (h ? w4 : w3) + (sidx & ~7));
+                return reinterpret_cast<const uint4*>(resid + (int)(h ? w4 : w3) + (sidx & ~7));
             };
-            // fast jobs (J5_FAST): one residual sample per lane (2-B load)
+            // fast jobs (J5_FAST): one residual sample per lane (2-B load); w3 / w4 already point
+            // at the pool, the residual or the zero block, and lanes past the TB read padding
             auto res_fast = [&](uint32_t w0, uint32_t w3, uint32_t w4) {
                 const bool pr = (w0 >> 15) & 3u;
-                const int lg = (int)((w0 >> 13) & 3u) + 2;
-                const int h = pr ? (lane >> 5) : 0;
-                const int hl = pr ? (lane & 31) : lane;
-                const bool cod = (w0 >> (28 + h)) & 1u;
-                const int16_t* base = ((w0 >> (26 + h)) & 1u) ? pool : resid;
-                const uint32_t o = cod ? (h ? w4 : w3) + (uint32_t)(hl < (1 << (2 * lg)) ? hl : 0) : 0u;
-                return base + o;
+                return resid + (int)(pr && lane >= 32 ? w4 : w3) + (pr ? (lane & 31) : lane);
             };
             // job records: 64 at a time into two VGPRs per lane, read per job with v_readlane
             // (scalar loads were measured slower: their lgkmcnt waits serialise with the LDS
@@ -664,9 +658,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             int r16n = 0;
             auto issue = [&](const JobS& j) {                    // residual loads of job j
                 if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) {        // 16x16 luma: 4 samples per lane
-                    const int16_t* base = ((j.w0 >> 26) & 1u) ? pool : resid;
-                    const uint32_t o = ((j.w0 >> 28) & 1u) ? j.w3 + 4u * (uint32_t)lane : 0u;
-                    const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(base + o));
+                    const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(resid + (int)j.w3 + 4 * lane));
                     ra = make_uint4(d.x, d.y, 0u, 0u);
                 } else if (j.w5 & J5_FAST) {
                     r16n = *gptr(res_fast(j.w0, j.w3, j.w4));

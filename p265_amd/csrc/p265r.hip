@@ -403,8 +403,11 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t o_ctus = off; off = align_up(off + sizeof(p265r_ctu) * nc * (size_t)n_pics, 256);
     const size_t o_tbs = off; off = align_up(off + sizeof(p265r_tb) * n_tbs_total, 256);
     // both pools padded by 64 B: the intra kernel reads fixed-shape 32-B runs
-    const size_t o_pool = off; off = align_up(off + sizeof(int16_t) * pool_total + 64, 256);
-    const size_t o_res = off; off = align_up(off + sizeof(int16_t) * pool_total + 64, 256);
+    // (the row kernel reads every residual relative to the residual pool: raw TBs at negative
+    // offsets into the coefficient pool, uncoded halves from a zero block after the residuals;
+    // fast jobs read one sample per lane, lanes past the TB up to 126 B beyond it)
+    const size_t o_pool = off; off = align_up(off + sizeof(int16_t) * pool_total + 256, 256);
+    const size_t o_res = off; off = align_up(off + sizeof(int16_t) * pool_total + 1024, 256);
     size_t o_jobs[RC_NUM];
     for (int c = 0; c < RC_NUM; ++c) { o_jobs[c] = off; off = align_up(off + sizeof(ResJob) * n_jobs[c], 256); }
     // intra jobs (same index space as the TB records) + per-CTU job counts
@@ -534,6 +537,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         dp.rec[1] = rec + align_up(plane_bytes[0], 256);
         dp.rec[2] = dp.rec[1] + align_up(plane_bytes[1], 256);
         dp.dbk_map = dbk ? dbase + o_map + nf_bytes * i : nullptr;
+        dp.pool_rel = -(int32_t)((o_res - o_pool) / sizeof(int16_t));
+        dp.zero_off = (uint32_t)pool_total;
         if (lf) {
             unsigned char* o = dbase + o_out + pic_plane_bytes * i;
             dp.out[0] = o;
