@@ -69,6 +69,12 @@ __device__ __forceinline__ T gload(const T* p) {
 __device__ __forceinline__ void* lds_ptr(uint32_t a) {
     return (void*)(__attribute__((address_space(3))) void*)(uintptr_t)a;
 }
+// LDS-typed pointers straight from a 32-bit LDS address: no generic round trip, so no
+// null-pointer remapping (v_cmp + v_cndmask per cast) in the fast paths
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ lds_u8* lds8(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
+__device__ __forceinline__ lds_u32* lds32(uint32_t a) { return (lds_u32*)(uintptr_t)a; }
 
 struct WaveLds {                 // one wave's private CTU state (6544 B)
     uint8_t  y[64 * 64];         // interior luma, stride 64
@@ -305,7 +311,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 // LDS write - no reference array in LDS and no divergent control flow.  r16 = this
 // lane's residual sample as loaded (ignored when the TB has none).
 template <int LOG2, bool PAIR>
-__device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
+__device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1,
                                            uint32_t w5, int r16, int lane) {
     constexpr int n = 1 << LOG2;
     constexpr int nn = n * n;
@@ -316,8 +322,6 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     const int xr = PAIR ? ((ofs - 4096) & 31) : (ofs & 63);
     const int yr = PAIR ? ((ofs - 4096) >> 5) : (ofs >> 6);
     constexpr int ist = PAIR ? 32 : 64;
-    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + ofs + half * 1024;
-    const uint8_t* const lcol = (PAIR ? L.cleft[half] : L.yleft) + yr;
     const int mode = (int)((w0 >> 17) & 63u);
     const int base = half * 32;                                  // first reference lane of this half
     // ---- gather: lane k <- reference sample Clip3(fa, la, k) -------------------------------
@@ -325,8 +329,9 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     const int k = min(hl, 4 * n);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
     const int sref = min(max(k, fa), la);
-    const uint32_t orgA = (uint32_t)(uintptr_t)org, lcolA = (uint32_t)(uintptr_t)lcol;
-    const uint32_t ltA = (uint32_t)(uintptr_t)line_top + xr;
+    const uint32_t orgA = lbase + (uint32_t)ofs + (uint32_t)half * 1024u;          // TB origin in the interior
+    const uint32_t lcolA = lbase + (uint32_t)(PAIR ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft)) + (uint32_t)yr;
+    const uint32_t ltA = line_top + (uint32_t)xr;
     // left refs k < 2n at lb - k * ls, top refs k > 2n at tb + k; the corner k = 2n follows the
     // left formula inside the CTU / left column and the top formula in the line buffer (yr = 0)
     const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
@@ -334,7 +339,7 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     const uint32_t tb = (yr == 0 ? ltA : orgA - ist) - 2 * n - 1;
     const int th = 2 * n + (yr > 0 ? 1 : 0);
     const uint32_t sa = tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
-    const int raw = (int)*reinterpret_cast<const uint8_t*>(lds_ptr(sa));
+    const int raw = (int)*lds8(sa);
     int v = (w0 & J_NONE) ? 128 : raw;
     if (!PAIR && LOG2 == 3 && ((w0 >> 24) & 3u)) {           // [1 2 1] (8.4.4.2.3), 8x8: never strong
         const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
@@ -394,26 +399,25 @@ __device__ __forceinline__ void recon_fast(WaveLds& L, const uint8_t* line_top, 
     // every lane stores (no exec-mask juggling): lanes without a sample of this job write a
     // private byte of the (here unused) reference scratch area
     const bool own = hl < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
-    const uint32_t da = own ? orgA + y * ist + x : (uint32_t)(uintptr_t)&L.ref[0][0] + lane;
-    const int res = ((w0 >> (28 + half)) & 1u) ? r16 : 0;      // coded: the loaded sample, else 0
-    *reinterpret_cast<uint8_t*>(lds_ptr(da)) = (uint8_t)clip_pel(pred + res, maxv);
+    const uint32_t da = own ? orgA + y * ist + x : lbase + (uint32_t)offsetof(WaveLds, ref) + lane;
+    // r16: the loaded sample (an uncoded half reads the zero block, intra_prep.h w3/w4)
+    *lds8(da) = (uint8_t)clip_pel(pred + r16, maxv);
     wave_sync();
 }
 
 // Fast 16x16 luma job (J5_FAST): as recon_fast, 65 reference samples (lane k holds
 // sample k, sample 64 is wave-uniform), 4 predicted samples per lane (a row quarter),
 // residual (4 samples) in rw.x / rw.y, one 4-byte LDS store per lane.
-__device__ __forceinline__ void recon_fast16(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
+__device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1,
                                              uint32_t w5, uint4 rw, int lane) {
     constexpr int n = 16, LOG2 = 4, ist = 64, maxv = 255;
     const int ofs = (int)(w0 & 0x1fffu);
     const int xr = ofs & 63, yr = ofs >> 6;
-    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + ofs;
-    const uint8_t* const lcol = L.yleft + yr;
     const int mode = (int)((w0 >> 17) & 63u);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
-    const uint32_t orgA = (uint32_t)(uintptr_t)org, lcolA = (uint32_t)(uintptr_t)lcol;
-    const uint32_t ltA = (uint32_t)(uintptr_t)line_top + xr;
+    const uint32_t orgA = lbase + (uint32_t)ofs;
+    const uint32_t lcolA = lbase + (uint32_t)offsetof(WaveLds, yleft) + (uint32_t)yr;
+    const uint32_t ltA = line_top + (uint32_t)xr;
     const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
     const int ls = xr == 0 ? 1 : ist;
     const uint32_t tb = (yr == 0 ? ltA : orgA - ist) - 2 * n - 1;
@@ -421,8 +425,8 @@ __device__ __forceinline__ void recon_fast16(WaveLds& L, const uint8_t* line_top
     auto addr = [&](int sref) { return tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u); };
     const bool none = (w0 & J_NONE) != 0;
     const int k = lane;
-    const int raw = (int)*reinterpret_cast<const uint8_t*>(lds_ptr(addr(min(max(k, fa), la))));
-    const int raw64 = (int)*reinterpret_cast<const uint8_t*>(lds_ptr(addr(min(max(4 * n, fa), la))));
+    const int raw = (int)*lds8(addr(min(max(k, fa), la)));
+    const int raw64 = (int)*lds8(addr(min(max(4 * n, fa), la)));
     int v = none ? 128 : raw;
     const int r64 = none ? 128 : __builtin_amdgcn_readfirstlane(raw64);     // reference sample 64 (end, unfiltered)
     if ((w0 >> 24) & 3u) {                                    // [1 2 1] (8.4.4.2.3)
@@ -492,15 +496,14 @@ __device__ __forceinline__ void recon_fast16(WaveLds& L, const uint8_t* line_top
             }
         }
     }
-    const bool coded = (w0 >> 28) & 1u;
-    uint32_t out = 0;
+    uint32_t out = 0;                                         // (an uncoded TB's residual is the zero block)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t wd = i < 2 ? rw.x : rw.y;
-        const int res = coded ? (int)(int16_t)(wd >> (16 * (i & 1))) : 0;
+        const int res = (int)(int16_t)(wd >> (16 * (i & 1)));
         out |= (uint32_t)clip_pel(pred[i] + res, maxv) << (8 * i);
     }
-    *reinterpret_cast<uint32_t*>(lds_ptr(orgA + y * ist + x0)) = out;
+    *lds32(orgA + y * ist + x0) = out;
     wave_sync();
 }
 
@@ -695,10 +698,10 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_FAST) {
                     switch (sel) {
-                        case 0: recon_fast<2, false>(LL, tlp, w0, w1, w5, c16, ln); break;
-                        case 1: recon_fast<3, false>(LL, tlp, w0, w1, w5, c16, ln); break;
-                        case 2: recon_fast16(LL, tlp, w0, w1, w5, ca, ln); break;
-                        default: recon_fast<2, true>(LL, tcp, w0, w1, w5, c16, ln); break;
+                        case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln); break;
+                        case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln); break;
+                        case 2: recon_fast16(lbase, tl, w0, w1, w5, ca, ln); break;
+                        default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln); break;
                     }
                 } else switch (sel) {
                     case 0: recon_job<2, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
