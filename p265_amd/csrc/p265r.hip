@@ -202,9 +202,18 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
         return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
+    auto fn = intra_rows_kernel<W>;
+    {
+        // every workgroup resident at once and holding a single picture: one slot is enough
+        // (a second picture would only wait for the first), and the smaller LDS footprint can
+        // fit one more workgroup per CU
+        int pc1 = 0;
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(1)));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc1, fn, 64 * W, lds_of(1)));
+        if (pc1 >= 1 && b->n_pics <= pc1 * ctx->num_cus) fs = 1;
+    }
     const size_t lds = lds_of(fs);
     if (lds > 160 * 1024) return P265R_EUNSUPPORTED;
-    auto fn = intra_rows_kernel<W>;
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds));
