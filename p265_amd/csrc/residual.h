@@ -109,6 +109,36 @@ __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// One N-point inverse transform, x[n] = sum_k M_N[k][n] c[k] with M_N[k][n] = kDCT32[k*32/N][n],
+// as an even/odd butterfly: even rows of the DCT matrix are symmetric (M_N[2k][n] = M_{N/2}[k][n]
+// for n < N/2), odd rows antisymmetric, so x[n] = E[n] + O[n] and x[N-1-n] = E[n] - O[n] with E the
+// N/2-point transform of the even coefficients.  Same integer sum as the matrix product (exact),
+// about N^2/3 instead of N^2 multiply-adds.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void inv_dct_eo(const int (&c)[N], int (&x)[N]) {
+    constexpr int H = N / 2;
+    constexpr int S = 32 / N;
+    int ce[H], ev[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) ce[k] = c[2 * k];
+    if constexpr (H == 2) {
+        ev[0] = kDCT32[0][0] * ce[0] + kDCT32[16][0] * ce[1];
+        ev[1] = kDCT32[0][1] * ce[0] + kDCT32[16][1] * ce[1];
+    } else {
+        inv_dct_eo<H>(ce, ev);
+    }
+#pragma unroll
+    for (int n = 0; n < H; ++n) {
+        int od = 0;
+#pragma unroll
+        for (int j = 0; j < H; ++j) od += kDCT32[(2 * j + 1) * S][n] * c[2 * j + 1];
+        x[n] = ev[n] + od;
+        x[N - 1 - n] = ev[n] - od;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // NxN, N = 8/16/32: N threads per TB (256/N TBs per 256-thread block).
 //   load row r (16-B vectors) -> dequant -> LDS [r][c]
 //   thread c: column transform (stage 1) + (e+64)>>7 clip -> LDS [k][c]
@@ -123,7 +153,6 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
     constexpr int N = 1 << LOG2;
     constexpr int TPB = 256 / N;                 // TBs per block
     constexpr int S = N + 2;                     // padded LDS row (odd dword stride)
-    constexpr int STEP = 32 / N;
     __shared__ int16_t tile[TPB][N * S];
     const int local = threadIdx.x / N;
     const int lane = threadIdx.x % N;            // row index (load/store) and column index (stage 1)
@@ -149,22 +178,19 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
     }
     __syncthreads();
     if (active) {
-        int col[N];
+        int col[N], e[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) col[k] = t[k * S + lane];
+        inv_dct_eo<N>(col, e);
 #pragma unroll
-        for (int y = 0; y < N; ++y) {
-            int e = 0;
-#pragma unroll
-            for (int k = 0; k < N; ++k) e += kDCT32[k * STEP][y] * col[k];
-            t[y * S + lane] = (int16_t)clamp16i((e + 64) >> 7);
-        }
+        for (int y = 0; y < N; ++y) t[y * S + lane] = (int16_t)clamp16i((e[y] + 64) >> 7);
     }
     __syncthreads();
     if (active) {
-        int row[N];
+        int row[N], xr[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) row[k] = t[lane * S + k];
+        inv_dct_eo<N>(row, xr);
         const int bd2 = 20 - bit_depth;
         const int rnd2 = 1 << (bd2 - 1);
 #pragma unroll
@@ -176,10 +202,7 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int x = v * 8 + h * 2 + q;
-                    int acc = 0;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) acc += kDCT32[k * STEP][x] * row[k];
-                    r2[q] = clamp16i((acc + rnd2) >> bd2);
+                    r2[q] = clamp16i((xr[x] + rnd2) >> bd2);
                 }
                 o[h] = (uint32_t)(uint16_t)r2[0] | ((uint32_t)(uint16_t)r2[1] << 16);
             }
