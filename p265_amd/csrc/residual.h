@@ -57,6 +57,24 @@ struct Dequant {
 template <bool DST>
 __device__ __forceinline__ int t4(int j, int i) { return DST ? kDST4[j][i] : kDCT32[j * 8][i]; }
 
+// o[n] = sum_k t4(k, n) * c[k] in butterfly form (same integer sums as the matrix product):
+// DST 29/55/74/84 factorisation, DCT even/odd.
+template <bool DST>
+__device__ __forceinline__ void inv4(const int (&c)[4], int (&o)[4]) {
+    if constexpr (DST) {
+        static_assert(kDST4[0][0] == 29 && kDST4[0][1] == 55 && kDST4[1][0] == 74 && kDST4[0][3] == 84, "DST matrix");
+        const int a = c[0] + c[2], b = c[2] + c[3], d = c[0] - c[3], e = 74 * c[1];
+        o[0] = 29 * a + 55 * b + e;
+        o[1] = 55 * d - 29 * b + e;
+        o[2] = 74 * (c[0] - c[2] + c[3]);
+        o[3] = 55 * a + 29 * d - e;
+    } else {
+        const int e0 = 64 * (c[0] + c[2]), e1 = 64 * (c[0] - c[2]);
+        const int o0 = 83 * c[1] + 36 * c[3], o1 = 36 * c[1] - 83 * c[3];
+        o[0] = e0 + o0; o[1] = e1 + o1; o[2] = e1 - o1; o[3] = e0 - o0;
+    }
+}
+
 template <bool DST>
 __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restrict__ pool,
                                                         int16_t* __restrict__ res,
@@ -80,13 +98,11 @@ __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restric
     int g[4][4];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {            // columns: e[y][x] = sum_j T[j][y] d[j][x]
+        const int cin[4] = {d[0][x], d[1][x], d[2][x], d[3][x]};
+        int e[4];
+        inv4<DST>(cin, e);
 #pragma unroll
-        for (int y = 0; y < 4; ++y) {
-            int e = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) e += t4<DST>(j, y) * d[j][x];
-            g[y][x] = clamp16i((e + 64) >> 7);
-        }
+        for (int y = 0; y < 4; ++y) g[y][x] = clamp16i((e[y] + 64) >> 7);
     }
     const int bd2 = 20 - bit_depth;
     const int rnd2 = 1 << (bd2 - 1);
@@ -94,13 +110,11 @@ __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restric
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
         int r[4];
+        const int rin[4] = {g[y][0], g[y][1], g[y][2], g[y][3]};
+        int acc[4];
+        inv4<DST>(rin, acc);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            int acc = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc += t4<DST>(j, x) * g[y][j];
-            r[x] = clamp16i((acc + rnd2) >> bd2);
-        }
+        for (int x = 0; x < 4; ++x) r[x] = clamp16i((acc[x] + rnd2) >> bd2);
         o[y * 2 + 0] = (uint32_t)(uint16_t)r[0] | ((uint32_t)(uint16_t)r[1] << 16);
         o[y * 2 + 1] = (uint32_t)(uint16_t)r[2] | ((uint32_t)(uint16_t)r[3] << 16);
     }
