@@ -160,9 +160,11 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     if (pic.flags & ~P265R_PIC_RECON_INPUT) return P265R_EINVAL;
     if ((pic.flags & P265R_PIC_RECON_INPUT) && (!pic.recon[0] || !pic.recon[1] || !pic.recon[2])) return P265R_EINVAL;
     const int ctb = 1 << p.ctb_log2_size;
+    const int max_tbs = 3 * (ctb / 4) * (ctb / 4) / 2;                  // all-4x4 luma + 4x4 chroma per 8x8
     for (int rs = 0; rs < ctx->n_ctus; ++rs) {
         const p265r_ctu& c = pic.ctus[rs];
         if ((uint64_t)c.tb_begin + c.tb_count > pic.n_tbs) return P265R_ERANGE;
+        if (c.tb_count > max_tbs) return P265R_EINVAL;                  // more TBs than 4x4 units
         for (int k = 0; k < 2; ++k) {
             const int v = ((c.deblock_offsets >> (4 * k)) & 15) ^ 8;   // biased: -6..6 -> 2..14
             if (v < 2 || v > 14) return P265R_EINVAL;
@@ -176,6 +178,7 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
         for (uint32_t i = c.tb_begin; i < c.tb_begin + c.tb_count; ++i) {
             const p265r_tb& t = pic.tbs[i];
             if (t.log2_size < 2 || t.log2_size > 5 || t.c_idx > 2 || t.pred_mode > 34) return P265R_EINVAL;
+            if (t.c_idx && t.log2_size > 4) return P265R_EINVAL;        // 4:2:0 chroma TBs are 4..16
             const int sub = t.c_idx ? 1 : 0;
             const int n = 1 << t.log2_size;
             const int xl = t.x << sub, yl = t.y << sub, nl = n << sub;
@@ -396,7 +399,10 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     size_t pool_base[N_POOLS];
     size_t pool_total = 0;
     for (int c = 0; c < N_POOLS; ++c) { pool_base[c] = pool_total; pool_total += pool_sz[c]; }
-    if (pool_total >= (1ull << 32)) return P265R_ERANGE;
+    // the row kernel addresses every residual as a signed 32-bit int16 offset relative to the
+    // residual pool: raw samples down to -(pool_total + 128) (coefficient pool + its pad), the
+    // zero block and the fast jobs' over-read up to pool_total + 512 + 64
+    if (pool_total + 2048 > (size_t)INT32_MAX) return P265R_ERANGE;
     // ---- device layout -----------------------------------------------------------
     const bool sao = ctx->params.sample_adaptive_offset != 0;
     bool dbk = false;

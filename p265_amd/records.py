@@ -148,6 +148,10 @@ def validate(params, pic: Picture):
     c = tbs["c_idx"].astype(np.int64)
     if ((lg < 2) | (lg > 5)).any() or (c > 2).any() or (tbs["pred_mode"] > 34).any():
         raise RecordError("TB size / component / mode out of range")
+    if ((c > 0) & (lg > 4)).any():
+        raise RecordError("4:2:0 chroma TB larger than 16x16")
+    if (pic.ctus["tb_count"].astype(np.int64) > 3 * (1 << (2 * (ctb_log2 - 2))) // 2).any():
+        raise RecordError("CTU lists more TBs than it has 4x4 units")
     sub = (c > 0).astype(np.int64)
     xl, yl = tbs["x"].astype(np.int64) << sub, tbs["y"].astype(np.int64) << sub
     nl = (1 << lg) << sub

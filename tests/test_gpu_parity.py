@@ -174,6 +174,65 @@ def test_invalid_records_rejected(recon_mod):
             ctx.decode([bad])
 
 
+def test_invalid_chroma_size_and_tb_count_rejected(recon_mod):
+    """A 32x32 chroma TB (impossible in 4:2:0) and a CTU listing more TBs than it has
+    4x4 units are EINVAL at upload, before anything reaches the GPU."""
+    from p265_amd import _lib
+    params = R.make_params(pic_width=64, pic_height=64)
+    pic = synth.make_picture(params, 3)
+    bad = R.Picture(ctus=pic.ctus.copy(), tbs=pic.tbs.copy(), coef=pic.coef)
+    k = int(np.nonzero(bad.tbs["c_idx"] > 0)[0][0])
+    bad.tbs["log2_size"][k] = 5
+    bad.tbs["x"][k] = bad.tbs["y"][k] = 0
+    bad.tbs["flags"][k] = 0
+    reps = (3 * 16 * 16 // 2 + 1) // len(pic.tbs) + 1
+    bad2 = R.Picture(ctus=pic.ctus.copy(), tbs=np.concatenate([pic.tbs] * reps), coef=pic.coef)
+    bad2.ctus["tb_count"][0] = 3 * 16 * 16 // 2 + 1
+    for b in (bad, bad2):
+        with pytest.raises(R.RecordError):
+            R.validate(params, b)
+        with recon_mod.ReconContext(params) as ctx:
+            with pytest.raises(_lib.P265RError) as ei:
+                ctx.decode([b])
+            assert ei.value.code == _lib.EINVAL
+
+
+def test_oversized_batch_returns_erange(recon_mod):
+    """A batch whose coded coefficients exceed the signed 32-bit residual offsets the row
+    kernel uses (2^31 int16) is refused with ERANGE at upload (no device allocation):
+    22 pictures of 8192x8192, every TB coded, all sharing one 1024-sample coefficient block."""
+    from p265_amd import _lib
+    params = R.make_params(pic_width=8192, pic_height=8192)
+    wc = hc = 8192 // 64
+    per_ctu = []
+    for c_idx, lg, step in ((0, 5, 32), (1, 4, 16), (2, 4, 16)):
+        for y in range(0, 64 >> (c_idx > 0), step):
+            for x in range(0, 64 >> (c_idx > 0), step):
+                per_ctu.append((x, y, lg, c_idx))
+    n = len(per_ctu)
+    tbs = np.zeros(wc * hc * n, R.TB_DTYPE)
+    ctus = np.zeros(wc * hc, R.CTU_DTYPE)
+    base = np.array(per_ctu, np.int64)
+    for rs in range(wc * hc):
+        cx, cy = (rs % wc) * 64, (rs // wc) * 64
+        sl = slice(rs * n, (rs + 1) * n)
+        sub = (base[:, 3] > 0).astype(np.int64)
+        tbs["x"][sl] = (cx >> sub) + base[:, 0]
+        tbs["y"][sl] = (cy >> sub) + base[:, 1]
+        tbs["log2_size"][sl] = base[:, 2]
+        tbs["c_idx"][sl] = base[:, 3]
+        ctus["tb_begin"][rs] = rs * n
+        ctus["tb_count"][rs] = n
+    tbs["flags"] = R.TB_CBF
+    tbs["qp"] = 30
+    pic = R.Picture(ctus=ctus, tbs=tbs, coef=np.zeros(1024, np.int16))
+    assert pic.n_coded_coef * 22 > 2 ** 31
+    with recon_mod.ReconContext(params) as ctx:
+        with pytest.raises(_lib.P265RError) as ei:
+            ctx.upload([pic] * 22)
+        assert ei.value.code == _lib.ERANGE
+
+
 def test_many_small_pictures_per_workgroup(recon_mod, schedule):
     """More pictures than resident workgroups: the row queue of one workgroup crosses
     picture boundaries (several pictures in flight per workgroup, line-buffer slots reused)."""

@@ -81,6 +81,17 @@ def test_validation_rejects_bad_records():
         R.validate(params, bad)
     with pytest.raises(R.RecordError):
         R.validate(params, R.Picture(pic.ctus[:0], pic.tbs, pic.coef))
+    # 4:2:0 chroma TBs stop at 16x16; a CTU cannot list more TBs than 1.5 per 4x4 luma unit
+    bad = R.Picture(pic.ctus.copy(), pic.tbs.copy(), pic.coef)
+    k = int(np.nonzero(bad.tbs["c_idx"] > 0)[0][0])
+    bad.tbs["log2_size"][k], bad.tbs["x"][k], bad.tbs["y"][k] = 5, 0, 0
+    with pytest.raises(R.RecordError):
+        R.validate(params, bad)
+    reps = 385 // len(pic.tbs) + 1
+    bad = R.Picture(pic.ctus.copy(), np.concatenate([pic.tbs] * reps), pic.coef)
+    bad.ctus["tb_count"][0] = 385
+    with pytest.raises(R.RecordError):
+        R.validate(params, bad)
 
 
 def test_synthetic_mix_follows_the_sanity_statistics():
