@@ -37,7 +37,7 @@ struct DevPic {                 // per picture, device-resident table
     uint8_t* out[3];            // SAO output planes (== rec when SAO is off)
     const uint8_t* nofilter;    // per 8x8 luma block or nullptr
     IntraJob* jobs;             // same index space as tbs (jobs of a CTU start at tb_begin)
-    uint32_t* jcount;           // per CTU: luma jobs | chroma jobs << 16 (luma listed first)
+    uint32_t* jcount;           // per CTU: luma jobs | chroma jobs << 16 (chroma listed first)
     uint8_t* dbk_map;           // per 8x8 luma block (loopfilter.h), nullptr without deblocking
     int32_t  pool_rel;          // residual pool element index of coefficient pool element 0 (<= 0)
     uint32_t zero_off;          // residual pool element index of a 256-sample zero block
@@ -53,6 +53,7 @@ struct Geo {                    // batch-uniform geometry
     int lf_tiles;
     int nf_w;                   // nofilter / deblocking map width (ceil(w/8))
     int cqp[2];                 // pps_cb_qp_offset, pps_cr_qp_offset (chroma deblocking)
+    int quad;                   // intra_prep_kernel merges luma 4x4 quads into one job (P265R_QUAD, default 1)
 };
 
 __constant__ int8_t  c_angle[35];

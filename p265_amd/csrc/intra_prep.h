@@ -38,6 +38,15 @@ namespace p265r {
 //      4x4 pairs, not PCM, whose available reference samples form ONE contiguous run
 //      [fa, la] of the linear order (or none): substitution (8.4.4.2.2) is then
 //      s = Clip3(fa, la, k).  fa bits 0..7, la bits 8..15.
+// Luma 4x4 QUAD job (w5 has J5_FAST | J5_QUAD): the four fast 4x4 luma TBs of one 8x8
+// region (blkIdx 0..3, consecutive in decode order) as ONE job, reconstructed in four
+// register-resident stages by intra_rows.h recon_quad:
+//  w0: [0,13) LDS offset of the region origin  [13,17) 0  [17,23) mode q0  [23,29) mode q1
+//      29 / 30: no reference available for q0 / q1
+//  w1: [0,6) mode q2  [6,12) mode q3  12 / 13: none for q2 / q3  [14,19) fa q0  [19,24) la q0
+//      [24,29) fa q1
+//  w2: [0,5) la q1  [5,10) fa q2  [10,15) la q2  [15,20) fa q3  [20,25) la q3
+//  w3, w4, w6, w7: residual offsets of q0, q1, q2, q3 (as w3 above)
 // (struct IntraJob: intra.h)
 
 enum : uint32_t {
@@ -45,15 +54,64 @@ enum : uint32_t {
     J_ALL = 1u << 30,
     J_NONE = 1u << 31,
     J5_FAST = 1u << 31,
+    J5_QUAD = 1u << 30,
 };
+
+struct LumaJobLds { uint32_t w0, w1, w2, w3, w5; };   // luma job words staged in LDS (w4 = zero_off)
+
+// the four jobs at slots s..s+3 are the fast 4x4 luma TBs of one 8x8 region, in z-order
+__device__ __forceinline__ bool quad_jobs(const LumaJobLds* j) {
+    const uint32_t o = j[0].w0 & 0x1fffu;
+    if ((o & 7u) || ((o >> 6) & 7u)) return false;                 // region origin on the 8x8 grid
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w0 = j[i].w0;
+        if (!(j[i].w5 & J5_FAST) || ((w0 >> 13) & 15u)) return false;     // fast, 4x4, luma
+        if ((w0 & 0x1fffu) != o + (uint32_t)((i & 1) * 4 + (i >> 1) * 256)) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j) {
+    uint32_t mode[4], none[4], fa[4], la[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mode[i] = (j[i].w0 >> 17) & 63u;
+        none[i] = j[i].w0 >> 31;
+        fa[i] = j[i].w5 & 31u;
+        la[i] = (j[i].w5 >> 8) & 31u;
+    }
+    IntraJob q;
+    q.w[0] = (j[0].w0 & 0x1fffu) | mode[0] << 17 | mode[1] << 23 | none[0] << 29 | none[1] << 30;
+    q.w[1] = mode[2] | mode[3] << 6 | none[2] << 12 | none[3] << 13 | fa[0] << 14 | la[0] << 19 | fa[1] << 24;
+    q.w[2] = la[1] | fa[2] << 5 | la[2] << 10 | fa[3] << 15 | la[3] << 20;
+    q.w[3] = j[0].w3;
+    q.w[4] = j[1].w3;
+    q.w[5] = J5_FAST | J5_QUAD;
+    q.w[6] = j[2].w3;
+    q.w[7] = j[3].w3;
+    return q;
+}
 
 __device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265r_tb& cr) {
     return cb.c_idx == 1 && cr.c_idx == 2 && cb.x == cr.x && cb.y == cr.y && cb.log2_size == cr.log2_size &&
            cb.pred_mode == cr.pred_mode && ((cb.flags ^ cr.flags) & P265R_TB_PCM) == 0;
 }
 
-// grid (CTUs, pictures), 64 threads: one wave per CTU walks its TBs 64 at a time.
+// grid (CTUs, pictures), 64 threads: one wave per CTU walks its TBs 64 at a time.  A CTU's
+// job list is [chroma jobs][luma jobs]: chroma jobs go straight to their slot, luma jobs are
+// staged in LDS (words 0, 1, 2, 3, 5; at most 256 per CTU, p265r.hip validate_picture) so
+// that luma 4x4 quads can be merged before the luma list is written, compacted.
+constexpr int kMaxCtuLuma = 256;
+__device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_off) {
+    IntraJob J;
+    J.w[0] = l.w0; J.w[1] = l.w1; J.w[2] = l.w2; J.w[3] = l.w3;
+    J.w[4] = zero_off; J.w[5] = l.w5; J.w[6] = J.w[7] = 0;
+    return J;
+}
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g) {
+    __shared__ LumaJobLds sj[kMaxCtuLuma];
+    __shared__ uint8_t head[kMaxCtuLuma];
     const DevPic P = pics[blockIdx.y];
     const int addr = blockIdx.x;
     const int lane = threadIdx.x;
@@ -70,15 +128,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const p265r_tb* tbs = P.tbs + me.tb_begin;
     IntraJob* jobs = P.jobs + me.tb_begin;
     const int cnt = me.tb_count;
-    // luma jobs first (decode order), then the chroma jobs (Cb+Cr pairs, unpaired Cb / Cr, in
-    // decode order): the row kernel runs the two components as independent row chains
+    // chroma jobs first (Cb+Cr pairs, unpaired Cb / Cr, decode order), then the luma jobs
+    // (decode order): the row kernel runs the two components as independent row chains
     // (4:2:0 intra prediction never reads across components)
-    int n_luma = 0;
-    for (int base = 0; base < cnt; base += 64) {
-        const int t = base + lane;
-        n_luma += __popcll(__ballot(t < cnt && tbs[t].c_idx == 0));
-    }
-    int out_l = 0, out_c = n_luma;
+    int out_l = 0, out_c = 0;
     auto rank = [&](unsigned long long m) {
         return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     };
@@ -156,12 +209,39 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             }
             J.w[5] = w5;
             J.w[6] = J.w[7] = 0;
-            uint4* dst = reinterpret_cast<uint4*>(jobs + slot);
+            if (kl) {
+                sj[slot] = LumaJobLds{J.w[0], J.w[1], J.w[2], J.w[3], J.w[5]};
+            } else {
+                uint4* dst = reinterpret_cast<uint4*>(jobs + slot);
+                dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
+                dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
+            }
+        }
+    }
+    const int n_luma = out_l, n_chroma = out_c;
+    __syncthreads();
+    // ---- luma 4x4 quads: slot s heads one when s..s+3 are its four fast TBs ------------------
+    for (int base = 0; base < n_luma; base += 64) {
+        const int s = base + lane;
+        if (s < n_luma) head[s] = (g.quad && s + 3 < n_luma && quad_jobs(sj + s)) ? 1 : 0;
+    }
+    __syncthreads();
+    int n_out = 0;
+    for (int base = 0; base < n_luma; base += 64) {
+        const int s = base + lane;
+        const bool valid = s < n_luma;
+        const bool absorbed = valid && ((s >= 1 && head[s - 1]) || (s >= 2 && head[s - 2]) || (s >= 3 && head[s - 3]));
+        const bool emit = valid && !absorbed;
+        const unsigned long long me_ = __ballot(emit);
+        if (emit) {
+            const IntraJob J = head[s] ? make_quad(sj + s) : luma_job(sj[s], P.zero_off);
+            uint4* dst = reinterpret_cast<uint4*>(jobs + n_chroma + n_out + rank(me_));
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
         }
+        n_out += __popcll(me_);
     }
-    if (lane == 0) P.jcount[addr] = (uint32_t)out_l | (uint32_t)(out_c - n_luma) << 16;
+    if (lane == 0) P.jcount[addr] = (uint32_t)n_out | (uint32_t)n_chroma << 16;
 }
 
 }  // namespace p265r

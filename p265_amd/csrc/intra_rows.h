@@ -303,6 +303,63 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
     wave_sync();
 }
 
+// Prediction (8.4.4.2.4-6) of sample (x, y) of a fast job: lane k of v holds reference
+// sample k of this lane's half (linear order of 8.4.4.2.2, substituted, filtered);
+// angw = intraPredAngle (int8, bits 0..7) | -invAngle << 8 (job word w1's layout).
+template <int LOG2, bool PAIR>
+__device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, int y, int k, int hl, int half) {
+    constexpr int n = 1 << LOG2;
+    constexpr int maxv = 255;
+    const int base = half * 32;                                  // first reference lane of this half
+    auto ref = [&](int i) { return __builtin_amdgcn_ds_bpermute((base + i) << 2, v); };
+    auto uref = [&](int i) {                                     // reference i of this lane's half, uniform per half
+        if constexpr (PAIR) {
+            const int c0 = __builtin_amdgcn_readlane(v, i), c1 = __builtin_amdgcn_readlane(v, i + 32);
+            return half ? c1 : c0;
+        } else {
+            return __builtin_amdgcn_readlane(v, i);
+        }
+    };
+    int pred;
+    if (mode == 0) {
+        const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
+        pred = (__mul24(n - 1 - x, lft) + __mul24(x + 1, uref(3 * n + 1)) + __mul24(n - 1 - y, top) +
+                __mul24(y + 1, uref(n - 1)) + n) >> (LOG2 + 1);
+    } else if (mode == 1) {
+        const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
+        const int dc = (wave_sum<PAIR>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
+        if (PAIR) {
+            pred = dc;
+        } else {                                                 // luma n < 32: edge smoothing
+            const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
+            // (lft + 2dc + top + 2) >> 2 at (0,0); one-sided (3dc + side + 2) >> 2 on row 0 / column 0
+            const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
+            pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
+        }
+    } else {
+        const int ang = (int)(int8_t)(angw & 0xffu);
+        const int inv = -(int)((angw >> 8) & 0x1fffu);
+        const bool vert = mode >= 18;
+        const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
+        const int pa = __mul24(along + 1, ang);
+        const int idx = pa >> 5, fact = pa & 31;
+        const int r0 = across + idx + 1;
+        auto refk = [&](int r) {                                 // r < 0: projected side reference (invAngle)
+            const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
+            return vert ? 2 * n + t : 2 * n - t;
+        };
+        const bool bflt = !PAIR && (mode == 26 || mode == 10);
+        const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : refk(r0 + 1);
+        const int a = ref(refk(r0)), b = ref(i1);
+        pred = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;   // = a when iFact = 0 (b then unused)
+        if (bflt) {                                              // modes 26 / 10, luma: boundary smoothing
+            const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
+            pred = (vert ? x : y) == 0 ? edge : pred;
+        }
+    }
+    return pred;
+}
+
 // Fast job (luma 4x4 / 8x8, Cb+Cr 4x4 pair; job word 5 has J5_FAST): the available
 // reference samples form one contiguous run [fa, la] of the linear order, so 8.4.4.2.2
 // substitution is a clamp.  Lane k gathers reference sample k straight into a register;
@@ -323,7 +380,6 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     const int yr = PAIR ? ((ofs - 4096) >> 5) : (ofs >> 6);
     constexpr int ist = PAIR ? 32 : 64;
     const int mode = (int)((w0 >> 17) & 63u);
-    const int base = half * 32;                                  // first reference lane of this half
     // ---- gather: lane k <- reference sample Clip3(fa, la, k) -------------------------------
     // (addresses as 32-bit LDS offsets, selected without branches; NONE: all refs = 128)
     const int k = min(hl, 4 * n);
@@ -347,55 +403,10 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
         const int f = (vl + 2 * v + vr + 2) >> 2;
         v = (k > 0 && k < 4 * n) ? f : v;                       // the two end samples stay unfiltered
     }
-    auto ref = [&](int i) { return __builtin_amdgcn_ds_bpermute((base + i) << 2, v); };
-    auto uref = [&](int i) {                                     // reference i of this lane's half, uniform per half
-        if constexpr (PAIR) {
-            const int c0 = __builtin_amdgcn_readlane(v, i), c1 = __builtin_amdgcn_readlane(v, i + 32);
-            return half ? c1 : c0;
-        } else {
-            return __builtin_amdgcn_readlane(v, i);
-        }
-    };
     // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------------------
     const int sidx = hl < nn ? hl : 0;
     const int x = sidx & (n - 1), y = sidx >> LOG2;
-    int pred;
-    if (mode == 0) {
-        const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
-        pred = (__mul24(n - 1 - x, lft) + __mul24(x + 1, uref(3 * n + 1)) + __mul24(n - 1 - y, top) +
-                __mul24(y + 1, uref(n - 1)) + n) >> (LOG2 + 1);
-    } else if (mode == 1) {
-        const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
-        const int dc = (wave_sum<PAIR>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
-        if (PAIR) {
-            pred = dc;
-        } else {                                                 // luma n < 32: edge smoothing
-            const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
-            // (lft + 2dc + top + 2) >> 2 at (0,0); one-sided (3dc + side + 2) >> 2 on row 0 / column 0
-            const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
-            pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
-        }
-    } else {
-        const int ang = (int)(int8_t)(w1 & 0xffu);
-        const int inv = -(int)((w1 >> 8) & 0x1fffu);
-        const bool vert = mode >= 18;
-        const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
-        const int pa = __mul24(along + 1, ang);
-        const int idx = pa >> 5, fact = pa & 31;
-        const int r0 = across + idx + 1;
-        auto refk = [&](int r) {                                 // r < 0: projected side reference (invAngle)
-            const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
-            return vert ? 2 * n + t : 2 * n - t;
-        };
-        const bool bflt = !PAIR && (mode == 26 || mode == 10);
-        const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : refk(r0 + 1);
-        const int a = ref(refk(r0)), b = ref(i1);
-        pred = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;   // = a when iFact = 0 (b then unused)
-        if (bflt) {                                              // modes 26 / 10, luma: boundary smoothing
-            const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
-            pred = (vert ? x : y) == 0 ? edge : pred;
-        }
-    }
+    const int pred = fast_pred<LOG2, PAIR>(mode, w1, v, x, y, k, hl, half);
     // every lane stores (no exec-mask juggling): lanes without a sample of this job write a
     // private byte of the (here unused) reference scratch area
     const bool own = hl < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
@@ -507,6 +518,86 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
     wave_sync();
 }
 
+// One stage of a luma 4x4 quad job (recon_quad): sub-TB Q of the 8x8 region.  Lane k of
+// the reference vector holds reference sample Clip3(fa, la, k) (8.4.4.2.2), taken from the
+// region's external samples (ext, gathered once per quad) or from the stages already
+// reconstructed (rec: lane = region sample y * 8 + x); the source of every reference index is
+// a compile-time affine map per stage.  Lanes of sub-TB Q then predict (fast_pred) and
+// reconstruct their sample into rec.
+template <int Q>
+__device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, bool none, int fa, int la,
+                                          uint32_t angw, int r16, int qid, int xs, int ys) {
+    constexpr int maxv = 255;
+    const int s = min(max(lane, fa), la);                        // substituted reference index
+    auto bp = [](int i, int src) { return __builtin_amdgcn_ds_bpermute(i << 2, src); };
+    int v;
+    if constexpr (Q == 0) {                                      // all external: corner e = 0, left e = 8 - s, top e = s + 4
+        v = bp(s <= 8 ? 8 - s : s + 4, ext);
+    } else if constexpr (Q == 1) {                               // left: q0's column x = 3; corner / top external
+        const int a = bp(59 - 8 * s, rec), b = bp(s + 8, ext);
+        v = s < 8 ? a : b;
+    } else if constexpr (Q == 2) {                               // left / corner external; top: q0 / q1 row y = 3
+        const int a = bp(12 - s, ext), b = bp(s + 15, rec);
+        v = s <= 8 ? a : b;
+    } else {                                                     // all internal (q2 column, q0 corner, q1 row)
+        v = bp(s <= 8 ? 91 - 8 * s : s + 19, rec);
+    }
+    v = none ? 128 : v;
+    const int pred = fast_pred<2, false>(mode, angw, v, xs, ys, lane, lane, 0);
+    return qid == Q ? clip_pel(pred + r16, maxv) : rec;
+}
+
+// Luma 4x4 quad job (J5_QUAD, intra_prep.h): the four fast 4x4 TBs of one 8x8 region in one
+// job.  Lane l = region sample (l & 7, l >> 3); the 25 external reference samples (column
+// x = -1, rows -1..11; row y = -1, columns 0..11) are read from LDS once, the four stages pass
+// their samples to each other through registers (ds_bpermute), and the region is written to
+// LDS once.  r16 = this lane's residual sample.
+__device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1, uint32_t w2,
+                                           int angtab, int r16, int lane) {
+    const int ofs = (int)(w0 & 0x1fffu);
+    const int X = ofs & 63, Y = ofs >> 6;
+    const uint32_t orgA = lbase + (uint32_t)ofs;
+    // ---- external references: e = 0..12 column x = -1 (row e - 1), e = 13..24 row y = -1 ------
+    const int e = min(lane, 24);
+    uint32_t ea;
+    if (e <= 12) {
+        const int r = min(Y - 1 + e, 63);                        // rows below the CTU: never available
+        const uint32_t in_left = X > 0 ? orgA - 1 + (uint32_t)((e - 1) * 64)
+                                       : lbase + (uint32_t)offsetof(WaveLds, yleft) + (uint32_t)r;
+        ea = r < 0 ? line_top + (uint32_t)(X - 1) : (X > 0 && Y - 1 + e > 63 ? lbase + 63 * 64 + (uint32_t)(X - 1) : in_left);
+    } else {
+        const int c = e - 13;
+        ea = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - 64 + (uint32_t)min(c, 63 - X);
+    }
+    const int ext = (int)*lds8(ea);
+    const int xs = lane & 3, ys = (lane >> 3) & 3;
+    const int qid = ((lane >> 4) & 2) | ((lane >> 2) & 1);
+    auto ang = [&](uint32_t m) { return (uint32_t)__builtin_amdgcn_readlane(angtab, (int)m); };
+    int rec = 0;
+    {
+        const uint32_t m = (w0 >> 17) & 63u;
+        rec = quad_stage<0>(rec, ext, lane, (int)m, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
+                            ang(m), r16, qid, xs, ys);
+    }
+    {
+        const uint32_t m = (w0 >> 23) & 63u;
+        rec = quad_stage<1>(rec, ext, lane, (int)m, (w0 >> 30) & 1u, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
+                            ang(m), r16, qid, xs, ys);
+    }
+    {
+        const uint32_t m = w1 & 63u;
+        rec = quad_stage<2>(rec, ext, lane, (int)m, (w1 >> 12) & 1u, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
+                            ang(m), r16, qid, xs, ys);
+    }
+    {
+        const uint32_t m = (w1 >> 6) & 63u;
+        rec = quad_stage<3>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
+                            ang(m), r16, qid, xs, ys);
+    }
+    *lds8(orgA + (uint32_t)((lane >> 3) * 64 + (lane & 7))) = (uint8_t)rec;
+    wave_sync();
+}
+
 template <int W>
 __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
@@ -531,6 +622,8 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
     const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
     unsigned char* lines = smem + 256 + prog_bytes + W * sizeof(WaveLds);
 
+    // intraPredAngle | -invAngle << 8 of mode m in lane m (quad jobs read theirs with v_readlane)
+    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)c_angle[lane] | (uint32_t)(-(int)c_inv_angle[lane]) << 8) : 0;
     if (threadIdx.x == 0) { ctl.next_row = 0; ctl.error = 0; }
     if (threadIdx.x < 32) ctl.done[threadIdx.x] = 0;
     for (int i = threadIdx.x; i < fs_count * units; i += 64 * W) prog[i] = -1;
@@ -616,11 +709,11 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             const int addr = cy * g.wc + cx;
             // this CTU's job list (intra_prep_kernel): first job = its first TB index
             const uint32_t tb_begin = uniform(gload(reinterpret_cast<const uint2*>(ctus + addr))).x;
-            // job counts: luma in bits 0..15 (listed first), chroma in bits 16..31 (intra_prep.h)
+            // job counts: luma in bits 0..15, chroma (listed first) in bits 16..31 (intra_prep.h)
             const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(*gptr(jcount + addr));
-            const int n_luma = (int)(jc & 0xffffu);
-            const int nt = comp ? (int)(jc >> 16) : n_luma;
-            const IntraJob* jl = jobs + tb_begin + (comp ? n_luma : 0);
+            const int n_chroma = (int)(jc >> 16);
+            const int nt = comp ? n_chroma : (int)(jc & 0xffffu);
+            const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
             // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr)
             const uint8_t* ltop_l = line_up + x0;
             const uint8_t* ltop_c = line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
@@ -659,8 +752,14 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             };
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
             int r16n = 0;
-            auto issue = [&](const JobS& j) {                    // residual loads of job j
-                if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) {        // 16x16 luma: 4 samples per lane
+            auto issue = [&](const JobS& j, int ji) {           // residual loads of job j (index ji)
+                if (j.w5 & J5_QUAD) {                                       // 4x4 quad: sample (x, y) of the 8x8 region
+                    const int l = ji & 63;
+                    const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane(rec1.z, l);
+                    const uint32_t w7 = (uint32_t)__builtin_amdgcn_readlane(rec1.w, l);
+                    const uint32_t o = (lane & 32) ? ((lane & 4) ? w7 : w6) : ((lane & 4) ? j.w4 : j.w3);
+                    r16n = *gptr(resid + (int)o + ((lane >> 1) & 12) + (lane & 3));
+                } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) { // 16x16 luma: 4 samples per lane
                     const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(resid + (int)j.w3 + 4 * lane));
                     ra = make_uint4(d.x, d.y, 0u, 0u);
                 } else if (j.w5 & J5_FAST) {
@@ -671,7 +770,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 }
             };
             JobS cur{0, 0, 0, 0, 0, 0};
-            if (nt) { refill(0); cur = sjob(0); issue(cur); }
+            if (nt) { refill(0); cur = sjob(0); issue(cur, 0); }
             for (int t = 0; t < nt; ++t) {
                 // next job's record and residual are fetched before this job runs; this job
                 // works on copies of its own (measured: issuing after the job is slower)
@@ -681,7 +780,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 if (t + 1 < nt) {
                     if (((t + 1) & 63) == 0) refill(t + 1);
                     cur = sjob(t + 1);
-                    issue(cur);
+                    issue(cur, t + 1);
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
                 // Opaque copies of the lane id and the LDS bases: keeps the compiler from
@@ -696,7 +795,9 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 WaveLds& LL = *reinterpret_cast<WaveLds*>(lds_ptr(lbase));
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
-                if (w5 & J5_FAST) {
+                if (w5 & J5_QUAD) {
+                    recon_quad(lbase, tl, w0, w1, w2, angtab, c16, ln);
+                } else if (w5 & J5_FAST) {
                     switch (sel) {
                         case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln); break;
                         case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln); break;

@@ -152,6 +152,9 @@ def validate(params, pic: Picture):
         raise RecordError("4:2:0 chroma TB larger than 16x16")
     if (pic.ctus["tb_count"].astype(np.int64) > 3 * (1 << (2 * (ctb_log2 - 2))) // 2).any():
         raise RecordError("CTU lists more TBs than it has 4x4 units")
+    cs = np.concatenate([[0], np.cumsum(tbs["c_idx"] == 0)])
+    if ((cs[end] - cs[begin]) > (1 << (2 * (ctb_log2 - 2)))).any():
+        raise RecordError("CTU lists more luma TBs than it has 4x4 units")
     sub = (c > 0).astype(np.int64)
     xl, yl = tbs["x"].astype(np.int64) << sub, tbs["y"].astype(np.int64) << sub
     nl = (1 << lg) << sub

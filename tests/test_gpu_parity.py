@@ -41,14 +41,16 @@ def _check(recon_mod, params, pics, label=""):
     return outs
 
 
-@pytest.fixture(params=["rows", "steps", "rows16", "rows4"])
+@pytest.fixture(params=["rows", "steps", "rows16", "rows4", "rows_noquad"])
 def schedule(request, monkeypatch):
-    """Both intra schedules (CU-local row pipeline with 4/8/16 waves, per-diagonal launches)."""
+    """Both intra schedules (CU-local row pipeline with 4/8/16 waves, with and without luma
+    4x4 quad jobs; per-diagonal launches)."""
     if request.param == "steps":
         monkeypatch.setenv("P265R_SCHEDULE", "steps")
     else:
         monkeypatch.setenv("P265R_SCHEDULE", "rows")
-        monkeypatch.setenv("P265R_ROW_WAVES", {"rows": "8", "rows16": "16", "rows4": "4"}[request.param])
+        monkeypatch.setenv("P265R_ROW_WAVES", {"rows": "8", "rows16": "16", "rows4": "4", "rows_noquad": "8"}[request.param])
+        monkeypatch.setenv("P265R_QUAD", "0" if request.param == "rows_noquad" else "1")
     return request.param
 
 
