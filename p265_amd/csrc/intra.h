@@ -53,7 +53,8 @@ struct Geo {                    // batch-uniform geometry
     int lf_tiles;
     int nf_w;                   // nofilter / deblocking map width (ceil(w/8))
     int cqp[2];                 // pps_cb_qp_offset, pps_cr_qp_offset (chroma deblocking)
-    int quad;                   // intra_prep_kernel merges luma 4x4 quads into one job (P265R_QUAD, default 1)
+    int quad;                   // intra_prep_kernel merges 4x4 quads into one job: bit 0 luma, bit 1 chroma
+                                // (P265R_QUAD, default 3)
 };
 
 __constant__ int8_t  c_angle[35];

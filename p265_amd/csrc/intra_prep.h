@@ -47,6 +47,13 @@ namespace p265r {
 //      [24,29) fa q1
 //  w2: [0,5) la q1  [5,10) fa q2  [10,15) la q2  [15,20) fa q3  [20,25) la q3
 //  w3, w4, w6, w7: residual offsets of q0, q1, q2, q3 (as w3 above)
+// Chroma 4x4 QUAD job (w5 has J5_FAST | J5_QUAD, w0 component mask 3): the four fast Cb+Cr
+// 4x4 pairs of one 8x8 chroma region (four consecutive TUs in decode order), reconstructed
+// by intra_rows.h recon_quad<true> with Cb and Cr packed in the 16-bit halves of one lane.
+//  w0: as the luma quad, [15,17) = 3, [0,13) LDS offset of the Cb region origin
+//  w1, w2: as the luma quad (modes, none bits, fa / la per sub-TB)
+//  w3: residual base offset; w4: 4-bit code per (sub-TB q, component h) at bit 8q + 4h,
+//      residual = w3 + 16 * code, code 15 = the zero block (w6 = zero_off)
 // (struct IntraJob: intra.h)
 
 enum : uint32_t {
@@ -93,16 +100,75 @@ __device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j) {
     return q;
 }
 
+struct ChromaJobLds { uint32_t w0, w1, w2, w3, w4, w5; };   // chroma job words staged in LDS
+
+// the four jobs at slots s..s+3 are fast Cb+Cr 4x4 pairs of one 8x8 chroma region, in z-order,
+// and their eight residuals are addressable as base + 16 * code (code <= 14; 15 = zero block):
+// coded chroma 4x4 TBs of one class are packed in decode order at upload (p265r.hip), so the
+// coded TBs of a region normally sit in consecutive 16-sample slots
+__device__ __forceinline__ bool cquad_jobs(const ChromaJobLds* j, uint32_t zero_off, uint32_t& base, uint32_t& codes) {
+    const uint32_t o = j[0].w0 & 0x1fffu;
+    if (o < 4096u || ((o - 4096u) & 7u) || (((o - 4096u) >> 5) & 7u)) return false;   // 8x8 chroma grid
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w0 = j[i].w0;
+        if (!(j[i].w5 & J5_FAST) || ((w0 >> 13) & 3u) || ((w0 >> 15) & 3u) != 3u) return false;   // fast 4x4 pair
+        if ((w0 & 0x1fffu) != o + (uint32_t)((i & 1) * 4 + (i >> 1) * 128)) return false;
+    }
+    int32_t mn = INT32_MAX;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t off = (i & 1) ? j[i >> 1].w4 : j[i >> 1].w3;
+        if (off != zero_off) mn = min(mn, (int32_t)off);
+    }
+    base = mn == INT32_MAX ? zero_off : (uint32_t)mn;
+    codes = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t off = (i & 1) ? j[i >> 1].w4 : j[i >> 1].w3;
+        uint32_t code = 15u;
+        if (off != zero_off) {
+            const int64_t d = (int64_t)(int32_t)off - mn;
+            if ((d & 15) || d > 14 * 16) return false;
+            code = (uint32_t)(d >> 4);
+        }
+        codes |= code << (4 * i);                 // i = 2q + h -> bit 8q + 4h
+    }
+    return true;
+}
+
+__device__ __forceinline__ IntraJob make_cquad(const ChromaJobLds* j, uint32_t base, uint32_t codes, uint32_t zero_off) {
+    uint32_t mode[4], none[4], fa[4], la[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mode[i] = (j[i].w0 >> 17) & 63u;
+        none[i] = j[i].w0 >> 31;
+        fa[i] = j[i].w5 & 31u;
+        la[i] = (j[i].w5 >> 8) & 31u;
+    }
+    IntraJob q;
+    q.w[0] = (j[0].w0 & 0x1fffu) | 3u << 15 | mode[0] << 17 | mode[1] << 23 | none[0] << 29 | none[1] << 30;
+    q.w[1] = mode[2] | mode[3] << 6 | none[2] << 12 | none[3] << 13 | fa[0] << 14 | la[0] << 19 | fa[1] << 24;
+    q.w[2] = la[1] | fa[2] << 5 | la[2] << 10 | fa[3] << 15 | la[3] << 20;
+    q.w[3] = base;
+    q.w[4] = codes;
+    q.w[5] = J5_FAST | J5_QUAD;
+    q.w[6] = zero_off;
+    q.w[7] = 0;
+    return q;
+}
+
 __device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265r_tb& cr) {
     return cb.c_idx == 1 && cr.c_idx == 2 && cb.x == cr.x && cb.y == cr.y && cb.log2_size == cr.log2_size &&
            cb.pred_mode == cr.pred_mode && ((cb.flags ^ cr.flags) & P265R_TB_PCM) == 0;
 }
 
 // grid (CTUs, pictures), 64 threads: one wave per CTU walks its TBs 64 at a time.  A CTU's
-// job list is [chroma jobs][luma jobs]: chroma jobs go straight to their slot, luma jobs are
-// staged in LDS (words 0, 1, 2, 3, 5; at most 256 per CTU, p265r.hip validate_picture) so
-// that luma 4x4 quads can be merged before the luma list is written, compacted.
+// job list is [chroma jobs][luma jobs]; both are staged in LDS (luma words 0, 1, 2, 3, 5, at
+// most 256 jobs per CTU; chroma words 0..5, at most 128; p265r.hip validate_picture) so that
+// luma and chroma 4x4 quads can be merged before the lists are written, compacted.
 constexpr int kMaxCtuLuma = 256;
+constexpr int kMaxCtuChroma = 128;
 __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_off) {
     IntraJob J;
     J.w[0] = l.w0; J.w[1] = l.w1; J.w[2] = l.w2; J.w[3] = l.w3;
@@ -111,7 +177,9 @@ __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_
 }
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g) {
     __shared__ LumaJobLds sj[kMaxCtuLuma];
+    __shared__ ChromaJobLds sc[kMaxCtuChroma];
     __shared__ uint8_t head[kMaxCtuLuma];
+    __shared__ uint8_t chead[kMaxCtuChroma];
     const DevPic P = pics[blockIdx.y];
     const int addr = blockIdx.x;
     const int lane = threadIdx.x;
@@ -209,23 +277,46 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             }
             J.w[5] = w5;
             J.w[6] = J.w[7] = 0;
-            if (kl) {
-                sj[slot] = LumaJobLds{J.w[0], J.w[1], J.w[2], J.w[3], J.w[5]};
-            } else {
-                uint4* dst = reinterpret_cast<uint4*>(jobs + slot);
-                dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
-                dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
-            }
+            if (kl) sj[slot] = LumaJobLds{J.w[0], J.w[1], J.w[2], J.w[3], J.w[5]};
+            else if (slot < kMaxCtuChroma) sc[slot] = ChromaJobLds{J.w[0], J.w[1], J.w[2], J.w[3], J.w[4], J.w[5]};
         }
     }
-    const int n_luma = out_l, n_chroma = out_c;
+    const int n_luma = out_l, n_chroma = min(out_c, kMaxCtuChroma);
     __syncthreads();
-    // ---- luma 4x4 quads: slot s heads one when s..s+3 are its four fast TBs ------------------
+    // ---- 4x4 quads: slot s heads one when s..s+3 are its four fast TBs / Cb+Cr pairs ---------
     for (int base = 0; base < n_luma; base += 64) {
         const int s = base + lane;
-        if (s < n_luma) head[s] = (g.quad && s + 3 < n_luma && quad_jobs(sj + s)) ? 1 : 0;
+        if (s < n_luma) head[s] = ((g.quad & 1) && s + 3 < n_luma && quad_jobs(sj + s)) ? 1 : 0;
+    }
+    for (int base = 0; base < n_chroma; base += 64) {
+        const int s = base + lane;
+        uint32_t qb, qc;
+        if (s < n_chroma) chead[s] = ((g.quad & 2) && s + 3 < n_chroma && cquad_jobs(sc + s, P.zero_off, qb, qc)) ? 1 : 0;
     }
     __syncthreads();
+    int c_out = 0;
+    for (int base = 0; base < n_chroma; base += 64) {
+        const int s = base + lane;
+        const bool valid = s < n_chroma;
+        const bool absorbed = valid && ((s >= 1 && chead[s - 1]) || (s >= 2 && chead[s - 2]) || (s >= 3 && chead[s - 3]));
+        const bool emit = valid && !absorbed;
+        const unsigned long long me_ = __ballot(emit);
+        if (emit) {
+            IntraJob J;
+            uint32_t qb = 0, qc = 0;
+            if (chead[s] && cquad_jobs(sc + s, P.zero_off, qb, qc)) {
+                J = make_cquad(sc + s, qb, qc, P.zero_off);
+            } else {
+                const ChromaJobLds& c = sc[s];
+                J.w[0] = c.w0; J.w[1] = c.w1; J.w[2] = c.w2; J.w[3] = c.w3;
+                J.w[4] = c.w4; J.w[5] = c.w5; J.w[6] = J.w[7] = 0;
+            }
+            uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + rank(me_));
+            dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
+            dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
+        }
+        c_out += __popcll(me_);
+    }
     int n_out = 0;
     for (int base = 0; base < n_luma; base += 64) {
         const int s = base + lane;
@@ -235,13 +326,13 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const unsigned long long me_ = __ballot(emit);
         if (emit) {
             const IntraJob J = head[s] ? make_quad(sj + s) : luma_job(sj[s], P.zero_off);
-            uint4* dst = reinterpret_cast<uint4*>(jobs + n_chroma + n_out + rank(me_));
+            uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + n_out + rank(me_));
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
         }
         n_out += __popcll(me_);
     }
-    if (lane == 0) P.jcount[addr] = (uint32_t)n_out | (uint32_t)n_chroma << 16;
+    if (lane == 0) P.jcount[addr] = (uint32_t)n_out | (uint32_t)c_out << 16;
 }
 
 }  // namespace p265r

@@ -518,13 +518,56 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
     wave_sync();
 }
 
-// One stage of a luma 4x4 quad job (recon_quad): sub-TB Q of the 8x8 region.  Lane k of
-// the reference vector holds reference sample Clip3(fa, la, k) (8.4.4.2.2), taken from the
+// Prediction (8.4.4.2.4-6) of sample (x, y) of a chroma 4x4 sub-TB of a chroma quad job, Cb
+// and Cr at once: every value is a packed pair (Cb bits 0..15, Cr bits 16..31).  Packed 8-bit
+// samples are < 2^24, so v_mul_u32_u24 weighs both halves with one multiply; every weighted
+// sum stays below 2^16 per half (planar 8 x 255, DC 8 x 255, angular 32 x 255 + 16), so
+// the halves never carry into each other and one shift + mask divides both.  Chroma (4:2:0)
+// has no DC / horizontal / vertical boundary smoothing.
+__device__ __forceinline__ uint32_t cquad_pred(int mode, uint32_t angw, uint32_t v, int x, int y, int k) {
+    constexpr int n = 4;
+    auto ref = [&](int i) { return (uint32_t)__builtin_amdgcn_ds_bpermute(i << 2, (int)v); };
+    auto uref = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); };
+    if (mode == 0) {
+        const uint32_t lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
+        const uint32_t s = __umul24(n - 1 - x, lft) + __umul24(x + 1, uref(3 * n + 1)) + __umul24(n - 1 - y, top) +
+                           __umul24(y + 1, uref(n - 1)) + 0x00040004u;
+        return (s >> 3) & 0x1fff1fffu;
+    }
+    if (mode == 1) {
+        const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
+        const uint32_t s = (uint32_t)wave_sum<false>(in ? (int)v : 0, 0) + 0x00040004u;
+        return (s >> 3) & 0x1fff1fffu;
+    }
+    const int ang = (int)(int8_t)(angw & 0xffu);
+    const int inv = -(int)((angw >> 8) & 0x1fffu);
+    const bool vert = mode >= 18;
+    const int along = vert ? y : x, across = vert ? x : y;
+    const int pa = __mul24(along + 1, ang);
+    const int idx = pa >> 5, fact = pa & 31;
+    const int r0 = across + idx + 1;
+    auto refk = [&](int r) {
+        const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
+        return vert ? 2 * n + t : 2 * n - t;
+    };
+    const uint32_t a = ref(refk(r0)), b = ref(refk(r0 + 1));
+    return ((__umul24(32 - fact, a) + __umul24(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+}
+
+// Clip1(pred + res) of both halves: pred packed (0..255 per half), res two int16 residuals
+__device__ __forceinline__ uint32_t cquad_recon(uint32_t pred, uint32_t res) {
+    const int cb = clip_pel((int)(pred & 0xffffu) + (int)(int16_t)(res & 0xffffu), 255);
+    const int cr = clip_pel((int)(pred >> 16) + ((int)res >> 16), 255);
+    return (uint32_t)cb | (uint32_t)cr << 16;
+}
+
+// One stage of a 4x4 quad job (recon_quad): sub-TB Q of the 8x8 region.  Lane k of the
+// reference vector holds reference sample Clip3(fa, la, k) (8.4.4.2.2), taken from the
 // region's external samples (ext, gathered once per quad) or from the stages already
 // reconstructed (rec: lane = region sample y * 8 + x); the source of every reference index is
 // a compile-time affine map per stage.  Lanes of sub-TB Q then predict (fast_pred) and
-// reconstruct their sample into rec.
-template <int Q>
+// reconstruct their sample into rec.  CH: chroma quad, every value a packed Cb | Cr << 16 pair.
+template <int Q, bool CH>
 __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, bool none, int fa, int la,
                                           uint32_t angw, int r16, int qid, int xs, int ys) {
     constexpr int maxv = 255;
@@ -542,59 +585,75 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     } else {                                                     // all internal (q2 column, q0 corner, q1 row)
         v = bp(s <= 8 ? 91 - 8 * s : s + 19, rec);
     }
-    v = none ? 128 : v;
-    const int pred = fast_pred<2, false>(mode, angw, v, xs, ys, lane, lane, 0);
-    return qid == Q ? clip_pel(pred + r16, maxv) : rec;
+    if constexpr (CH) {
+        v = none ? 0x00800080 : v;
+        const uint32_t pred = cquad_pred(mode, angw, (uint32_t)v, xs, ys, lane);
+        return qid == Q ? (int)cquad_recon(pred, (uint32_t)r16) : rec;
+    } else {
+        v = none ? 128 : v;
+        const int pred = fast_pred<2, false>(mode, angw, v, xs, ys, lane, lane, 0);
+        return qid == Q ? clip_pel(pred + r16, maxv) : rec;
+    }
 }
 
-// Luma 4x4 quad job (J5_QUAD, intra_prep.h): the four fast 4x4 TBs of one 8x8 region in one
-// job.  Lane l = region sample (l & 7, l >> 3); the 25 external reference samples (column
-// x = -1, rows -1..11; row y = -1, columns 0..11) are read from LDS once, the four stages pass
-// their samples to each other through registers (ds_bpermute), and the region is written to
-// LDS once.  r16 = this lane's residual sample.
+// 4x4 QUAD job (J5_QUAD, intra_prep.h): the four fast 4x4 TBs of one 8x8 luma region (CH =
+// false), or the four Cb+Cr 4x4 pairs of one 8x8 chroma region (CH = true), in one job.  Lane
+// l = region sample (l & 7, l >> 3); the 25 external reference samples (column x = -1, rows
+// -1..11; row y = -1, columns 0..11) are read from LDS once (chroma: Cb by lanes 0-24, Cr by
+// lanes 32-56, then packed into lanes 0-24), the four stages pass their samples to each other
+// through registers (ds_bpermute), and the region is written to LDS once.  r16 = this lane's
+// residual sample (chroma: the packed Cb | Cr << 16 pair); line_top = the row above the CTU
+// for this lane's component (chroma: lane half 0 Cb, 1 Cr).
+template <bool CH>
 __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1, uint32_t w2,
                                            int angtab, int r16, int lane) {
+    constexpr int ist = CH ? 32 : 64, last = ist - 1;           // interior stride, last row / column
     const int ofs = (int)(w0 & 0x1fffu);
-    const int X = ofs & 63, Y = ofs >> 6;
-    const uint32_t orgA = lbase + (uint32_t)ofs;
+    const int X = CH ? ((ofs - 4096) & 31) : (ofs & 63), Y = CH ? ((ofs - 4096) >> 5) : (ofs >> 6);
+    const int half = CH ? (lane >> 5) : 0;
+    const uint32_t orgA = lbase + (uint32_t)ofs + (uint32_t)(half * 1024);
+    const uint32_t leftA = lbase + (uint32_t)(CH ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft));
     // ---- external references: e = 0..12 column x = -1 (row e - 1), e = 13..24 row y = -1 ------
-    const int e = min(lane, 24);
+    const int e = min(CH ? (lane & 31) : lane, 24);
     uint32_t ea;
     if (e <= 12) {
-        const int r = min(Y - 1 + e, 63);                        // rows below the CTU: never available
-        const uint32_t in_left = X > 0 ? orgA - 1 + (uint32_t)((e - 1) * 64)
-                                       : lbase + (uint32_t)offsetof(WaveLds, yleft) + (uint32_t)r;
-        ea = r < 0 ? line_top + (uint32_t)(X - 1) : (X > 0 && Y - 1 + e > 63 ? lbase + 63 * 64 + (uint32_t)(X - 1) : in_left);
+        const int r = min(Y - 1 + e, last);                      // rows below the CTU: never available
+        const uint32_t in_left = X > 0 ? orgA - 1 + (uint32_t)((e - 1) * ist) : leftA + (uint32_t)r;
+        ea = r < 0 ? line_top + (uint32_t)(X - 1)
+                   : (X > 0 && Y - 1 + e > last ? orgA - (uint32_t)(Y * ist) + (uint32_t)(last * ist) - 1 : in_left);
     } else {
         const int c = e - 13;
-        ea = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - 64 + (uint32_t)min(c, 63 - X);
+        ea = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - ist + (uint32_t)min(c, last - X);
     }
-    const int ext = (int)*lds8(ea);
+    int ext = (int)*lds8(ea);
+    if constexpr (CH) ext |= __builtin_amdgcn_ds_bpermute(((lane + 32) & 63) << 2, ext) << 16;   // Cb | Cr << 16
     const int xs = lane & 3, ys = (lane >> 3) & 3;
     const int qid = ((lane >> 4) & 2) | ((lane >> 2) & 1);
     auto ang = [&](uint32_t m) { return (uint32_t)__builtin_amdgcn_readlane(angtab, (int)m); };
     int rec = 0;
     {
         const uint32_t m = (w0 >> 17) & 63u;
-        rec = quad_stage<0>(rec, ext, lane, (int)m, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
-                            ang(m), r16, qid, xs, ys);
+        rec = quad_stage<0, CH>(rec, ext, lane, (int)m, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
+                                ang(m), r16, qid, xs, ys);
     }
     {
         const uint32_t m = (w0 >> 23) & 63u;
-        rec = quad_stage<1>(rec, ext, lane, (int)m, (w0 >> 30) & 1u, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
-                            ang(m), r16, qid, xs, ys);
+        rec = quad_stage<1, CH>(rec, ext, lane, (int)m, (w0 >> 30) & 1u, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
+                                ang(m), r16, qid, xs, ys);
     }
     {
         const uint32_t m = w1 & 63u;
-        rec = quad_stage<2>(rec, ext, lane, (int)m, (w1 >> 12) & 1u, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
-                            ang(m), r16, qid, xs, ys);
+        rec = quad_stage<2, CH>(rec, ext, lane, (int)m, (w1 >> 12) & 1u, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
+                                ang(m), r16, qid, xs, ys);
     }
     {
         const uint32_t m = (w1 >> 6) & 63u;
-        rec = quad_stage<3>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
-                            ang(m), r16, qid, xs, ys);
+        rec = quad_stage<3, CH>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
+                                ang(m), r16, qid, xs, ys);
     }
-    *lds8(orgA + (uint32_t)((lane >> 3) * 64 + (lane & 7))) = (uint8_t)rec;
+    const uint32_t da = lbase + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
+    *lds8(da) = (uint8_t)rec;
+    if constexpr (CH) *lds8(da + 1024) = (uint8_t)(rec >> 16);
     wave_sync();
 }
 
@@ -753,7 +812,17 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
             int r16n = 0;
             auto issue = [&](const JobS& j, int ji) {           // residual loads of job j (index ji)
-                if (j.w5 & J5_QUAD) {                                       // 4x4 quad: sample (x, y) of the 8x8 region
+                if ((j.w5 & J5_QUAD) && ((j.w0 >> 15) & 3u)) {              // chroma quad: Cb | Cr << 16 of (x, y)
+                    const int l = ji & 63;
+                    const int zero = __builtin_amdgcn_readlane(rec1.z, l);      // w6 = zero_off
+                    const int q = ((lane >> 4) & 2) | ((lane >> 2) & 1);
+                    const uint32_t codes = j.w4 >> (8 * q);
+                    const int i = ((lane >> 1) & 12) + (lane & 3);          // sample index in the 4x4 sub-TB
+                    auto at = [&](uint32_t code) { return (code == 15u ? zero : (int)j.w3 + (int)(code << 4)) + i; };
+                    const uint32_t cb = (uint16_t)*gptr(resid + at(codes & 15u));
+                    const uint32_t cr = (uint16_t)*gptr(resid + at((codes >> 4) & 15u));
+                    r16n = (int)(cb | cr << 16);
+                } else if (j.w5 & J5_QUAD) {                                // 4x4 quad: sample (x, y) of the 8x8 region
                     const int l = ji & 63;
                     const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane(rec1.z, l);
                     const uint32_t w7 = (uint32_t)__builtin_amdgcn_readlane(rec1.w, l);
@@ -796,7 +865,8 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_QUAD) {
-                    recon_quad(lbase, tl, w0, w1, w2, angtab, c16, ln);
+                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tc, w0, w1, w2, angtab, c16, ln);
+                    else recon_quad<false>(lbase, tl, w0, w1, w2, angtab, c16, ln);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
                         case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln); break;

@@ -175,10 +175,11 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
             if (c.sao_type[k] == 1 && c.sao_class[k] > 31) return P265R_EINVAL;
         }
         const int cx0 = (rs % g.wc) * ctb, cy0 = (rs / g.wc) * ctb;
-        int n_luma = 0;
+        int n_luma = 0, n_chroma = 0;
         for (uint32_t i = c.tb_begin; i < c.tb_begin + c.tb_count; ++i) {
             const p265r_tb& t = pic.tbs[i];
             if (t.c_idx == 0 && ++n_luma > (ctb / 4) * (ctb / 4)) return P265R_EINVAL;   // intra_prep.h kMaxCtuLuma
+            if (t.c_idx && ++n_chroma > 2 * (ctb / 8) * (ctb / 8)) return P265R_EINVAL;  // kMaxCtuChroma
             if (t.log2_size < 2 || t.log2_size > 5 || t.c_idx > 2 || t.pred_mode > 34) return P265R_EINVAL;
             if (t.c_idx && t.log2_size > 4) return P265R_EINVAL;        // 4:2:0 chroma TBs are 4..16
             const int sub = t.c_idx ? 1 : 0;
@@ -319,8 +320,8 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.nf_w = (g.w + 7) / 8;
     g.cqp[0] = p.pps_cb_qp_offset;
     g.cqp[1] = p.pps_cr_qp_offset;
-    g.quad = 1;
-    if (const char* v = std::getenv("P265R_QUAD")) g.quad = v[0] != '0';
+    g.quad = 3;
+    if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 3;
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';

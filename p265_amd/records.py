@@ -155,6 +155,9 @@ def validate(params, pic: Picture):
     cs = np.concatenate([[0], np.cumsum(tbs["c_idx"] == 0)])
     if ((cs[end] - cs[begin]) > (1 << (2 * (ctb_log2 - 2)))).any():
         raise RecordError("CTU lists more luma TBs than it has 4x4 units")
+    cc = np.concatenate([[0], np.cumsum(tbs["c_idx"] != 0)])
+    if ((cc[end] - cc[begin]) > 2 * (1 << (2 * (ctb_log2 - 3)))).any():
+        raise RecordError("CTU lists more chroma TBs than it has 4x4 chroma units")
     sub = (c > 0).astype(np.int64)
     xl, yl = tbs["x"].astype(np.int64) << sub, tbs["y"].astype(np.int64) << sub
     nl = (1 << lg) << sub

@@ -177,8 +177,8 @@ def test_invalid_records_rejected(recon_mod):
 
 
 def test_invalid_chroma_size_and_tb_count_rejected(recon_mod):
-    """A 32x32 chroma TB (impossible in 4:2:0) and a CTU listing more TBs than it has
-    4x4 units are EINVAL at upload, before anything reaches the GPU."""
+    """A 32x32 chroma TB (impossible in 4:2:0) and a CTU listing more TBs (or chroma TBs)
+    than it has 4x4 units are EINVAL at upload, before anything reaches the GPU."""
     from p265_amd import _lib
     params = R.make_params(pic_width=64, pic_height=64)
     pic = synth.make_picture(params, 3)
@@ -190,7 +190,8 @@ def test_invalid_chroma_size_and_tb_count_rejected(recon_mod):
     reps = (3 * 16 * 16 // 2 + 1) // len(pic.tbs) + 1
     bad2 = R.Picture(ctus=pic.ctus.copy(), tbs=np.concatenate([pic.tbs] * reps), coef=pic.coef)
     bad2.ctus["tb_count"][0] = 3 * 16 * 16 // 2 + 1
-    for b in (bad, bad2):
+    from test_records import chroma_overfull
+    for b in (bad, bad2, chroma_overfull(pic)):
         with pytest.raises(R.RecordError):
             R.validate(params, b)
         with recon_mod.ReconContext(params) as ctx:

@@ -92,6 +92,21 @@ def test_validation_rejects_bad_records():
     bad.ctus["tb_count"][0] = 385
     with pytest.raises(R.RecordError):
         R.validate(params, bad)
+    # ... nor more chroma TBs than 4x4 chroma units (128 at CTB 64: intra_prep.h kMaxCtuChroma)
+    with pytest.raises(R.RecordError):
+        R.validate(params, chroma_overfull(pic))
+
+
+def chroma_overfull(pic):
+    """CTU 0 lists 129 chroma 4x4 TBs (all at its origin) and nothing else."""
+    k = int(np.nonzero((pic.tbs["c_idx"] == 1) & (pic.ctus["tb_begin"][0] <= np.arange(len(pic.tbs))))[0][0])
+    one = pic.tbs[k:k + 1].copy()
+    one["log2_size"], one["x"], one["y"], one["flags"] = 2, 0, 0, 0
+    tbs = np.concatenate([np.repeat(one, 129), pic.tbs])
+    ctus = pic.ctus.copy()
+    ctus["tb_begin"] += 129
+    ctus["tb_begin"][0], ctus["tb_count"][0] = 0, 129
+    return R.Picture(ctus, tbs, pic.coef)
 
 
 def test_synthetic_mix_follows_the_sanity_statistics():
