@@ -53,7 +53,10 @@ struct Geo {                    // batch-uniform geometry
     int lf_tiles;
     int nf_w;                   // nofilter / deblocking map width (ceil(w/8))
     int cqp[2];                 // pps_cb_qp_offset, pps_cr_qp_offset (chroma deblocking)
-    int quad;                   // intra_prep_kernel merges 4x4 quads into one job: bit 0 luma, bit 1 chroma
+    int fair;                   // intra_rows_kernel: the workgroup behind its CU partner raises its priority
+                                // (P265R_FAIR, default 1)
+    int quad;                   // intra_prep_kernel merges 4x4 quads into one job: bit 0 luma, bit 1 chroma;
+                                // bit 2 (A/B only): Cb+Cr 8x8 pairs take the general path
                                 // (P265R_QUAD, default 3)
 };
 

@@ -35,7 +35,7 @@ namespace p265r {
 //      the residual pool for every kind of TB: bypass/PCM samples at a negative offset into
 //      the coefficient pool (DevPic::pool_rel), uncoded halves at a zero block (zero_off)
 //  w5: fast-path job (intra_rows.h recon_fast*): bit 31 set for luma 4x4 .. 16x16 and Cb+Cr
-//      4x4 pairs, not PCM, whose available reference samples form ONE contiguous run
+//      4x4 / 8x8 pairs, not PCM, whose available reference samples form ONE contiguous run
 //      [fa, la] of the linear order (or none): substitution (8.4.4.2.2) is then
 //      s = Clip3(fa, la, k).  fa bits 0..7, la bits 8..15.
 // Luma 4x4 QUAD job (w5 has J5_FAST | J5_QUAD): the four fast 4x4 luma TBs of one 8x8
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
 #ifndef P265R_FAST16
 #define P265R_FAST16 1
 #endif
-            const bool fast_size = (c == 0 && n <= (P265R_FAST16 ? 16 : 8)) || (cm == 3u && n == 4);
+            const bool fast_size = (c == 0 && n <= (P265R_FAST16 ? 16 : 8)) || (cm == 3u && n <= (g.quad & 4 ? 4 : 8));
             if (fast_size && !(f0 & P265R_TB_PCM)) {
                 const int US = c ? 1 : 2;
                 if (m == 0) {

@@ -76,20 +76,41 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ lds_u8* lds8(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
 __device__ __forceinline__ lds_u32* lds32(uint32_t a) { return (lds_u32*)(uintptr_t)a; }
 
-struct WaveLds {                 // one wave's private CTU state (6544 B)
-    uint8_t  y[64 * 64];         // interior luma, stride 64
-    uint8_t  c[2][32 * 32];      // interior chroma, stride 32
-    uint8_t  yleft[64];          // right column of the previous CTU of this row
-    uint8_t  cleft[2][32];
-    uint8_t  ref[2][136];        // raw / final linear reference arrays (8-bit samples)
+struct WaveLds {                 // one wave's private CTU state (4432 B): a wave holds one row
+    uint8_t  ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
+    union {                      // ref: raw / final linear reference arrays (8-bit samples)
+        struct {
+            uint8_t y[64 * 64];          // interior luma, stride 64
+            uint8_t yleft[64];           // right column of the previous CTU of this row
+        };
+        struct {
+            uint8_t c[2][32 * 32];       // interior chroma, stride 32
+            uint8_t cleft[2][32];
+        };
+    };
 };
+// job word w0 addresses a TB origin as yr * 64 + xr (luma) or 4096 + yr * 32 + xr (chroma,
+// intra_prep.h); WaveLds byte of that origin = w0 offset + kOrg[chroma]
+constexpr uint32_t kOrgL = offsetof(WaveLds, y);
+constexpr uint32_t kOrgC = (uint32_t)offsetof(WaveLds, c) - 4096u;
 
 struct RowCtrl {                 // 256 B at the start of dynamic LDS
     int next_row;
     int error;
     int done[32];                // per picture slot: rows completed (monotonic over generations)
-    int pad[30];
+    int cu_slot;                 // this workgroup's per-CU slot (Geo::fair) and its rank there
+    int cu_rank;
+    int pad[28];
 };
+
+// Fair sharing of a CU between the row kernel's workgroups (Geo::fair).  Two workgroups share
+// each CU; the SIMDs arbitrate vector issue by priority, then age, so the older one runs ahead
+// and finishes ~25 % earlier (measured: 11.9 vs 14.9 M cycles per 1080p picture), leaving the CU
+// half empty for the younger one's tail.  Each workgroup takes a rank in its CU's slot (one
+// atomic add at start; slot = XCC id x 128 + CU / SH / SE id), publishes the rows it has
+// dequeued, and at every row start runs at priority 1 while it is behind its partner.
+constexpr int kRowCuSlots = 1024;
+struct RowCuSlot { int count; int prog[3]; };
 // Dynamic LDS layout: [RowCtrl 256 B][prog: fs x hc ints][W x WaveLds][fs x 2 line buffers]
 // prog[slot][cy] = (local picture index & 0xffff) << 16 | CTUs done.
 
@@ -142,7 +163,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
     const int xr = PAIR ? ((ofs - 4096) & 31) : (ofs & 63);
     const int yr = PAIR ? ((ofs - 4096) >> 5) : (ofs >> 6);
     constexpr int ist = PAIR ? 32 : 64;
-    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + ofs + half * 1024;     // TB origin in the interior
+    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + (PAIR ? kOrgC : kOrgL) + ofs + half * 1024;   // TB origin
     const uint8_t* const lcol = (PAIR ? L.cleft[half] : L.yleft) + yr;
     const int mode = (int)((w0 >> 17) & 63u);
     const bool own = hl * S < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
@@ -385,7 +406,7 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     const int k = min(hl, 4 * n);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
     const int sref = min(max(k, fa), la);
-    const uint32_t orgA = lbase + (uint32_t)ofs + (uint32_t)half * 1024u;          // TB origin in the interior
+    const uint32_t orgA = lbase + (PAIR ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)half * 1024u;   // TB origin
     const uint32_t lcolA = lbase + (uint32_t)(PAIR ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft)) + (uint32_t)yr;
     const uint32_t ltA = line_top + (uint32_t)xr;
     // left refs k < 2n at lb - k * ls, top refs k > 2n at tb + k; the corner k = 2n follows the
@@ -426,7 +447,7 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
     const int xr = ofs & 63, yr = ofs >> 6;
     const int mode = (int)((w0 >> 17) & 63u);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
-    const uint32_t orgA = lbase + (uint32_t)ofs;
+    const uint32_t orgA = lbase + kOrgL + (uint32_t)ofs;
     const uint32_t lcolA = lbase + (uint32_t)offsetof(WaveLds, yleft) + (uint32_t)yr;
     const uint32_t ltA = line_top + (uint32_t)xr;
     const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
@@ -518,26 +539,29 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
     wave_sync();
 }
 
-// Prediction (8.4.4.2.4-6) of sample (x, y) of a chroma 4x4 sub-TB of a chroma quad job, Cb
-// and Cr at once: every value is a packed pair (Cb bits 0..15, Cr bits 16..31).  Packed 8-bit
-// samples are < 2^24, so v_mul_u32_u24 weighs both halves with one multiply; every weighted
-// sum stays below 2^16 per half (planar 8 x 255, DC 8 x 255, angular 32 x 255 + 16), so
-// the halves never carry into each other and one shift + mask divides both.  Chroma (4:2:0)
-// has no DC / horizontal / vertical boundary smoothing.
-__device__ __forceinline__ uint32_t cquad_pred(int mode, uint32_t angw, uint32_t v, int x, int y, int k) {
-    constexpr int n = 4;
+// Chroma prediction (8.4.4.2.4-6) of sample (x, y) of an nTbS = 2^LOG2 Cb+Cr pair, Cb and Cr
+// at once: every value is a packed pair (Cb bits 0..15, Cr bits 16..31).  Packed 8-bit samples
+// are < 2^24, so v_mul_u32_u24 weighs both halves with one multiply; every weighted sum stays
+// below 2^16 per half (planar / DC 2n x 255 + n, angular 32 x 255 + 16), so the halves never
+// carry into each other and one shift + mask divides both.  Lane k of v holds reference k of
+// 8.4.4.2.2's linear order.  Chroma (4:2:0) has no DC / horizontal / vertical boundary smoothing.
+template <int LOG2>
+__device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, int x, int y, int k) {
+    constexpr int n = 1 << LOG2;
+    constexpr uint32_t rnd = (uint32_t)n * 0x00010001u;
+    constexpr uint32_t msk = (0xffffu >> (LOG2 + 1)) * 0x00010001u;
     auto ref = [&](int i) { return (uint32_t)__builtin_amdgcn_ds_bpermute(i << 2, (int)v); };
     auto uref = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); };
     if (mode == 0) {
         const uint32_t lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
         const uint32_t s = __umul24(n - 1 - x, lft) + __umul24(x + 1, uref(3 * n + 1)) + __umul24(n - 1 - y, top) +
-                           __umul24(y + 1, uref(n - 1)) + 0x00040004u;
-        return (s >> 3) & 0x1fff1fffu;
+                           __umul24(y + 1, uref(n - 1)) + rnd;
+        return (s >> (LOG2 + 1)) & msk;
     }
     if (mode == 1) {
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
-        const uint32_t s = (uint32_t)wave_sum<false>(in ? (int)v : 0, 0) + 0x00040004u;
-        return (s >> 3) & 0x1fff1fffu;
+        const uint32_t s = (uint32_t)wave_sum<false>(in ? (int)v : 0, 0) + rnd;
+        return (s >> (LOG2 + 1)) & msk;
     }
     const int ang = (int)(int8_t)(angw & 0xffu);
     const int inv = -(int)((angw >> 8) & 0x1fffu);
@@ -559,6 +583,40 @@ __device__ __forceinline__ uint32_t cquad_recon(uint32_t pred, uint32_t res) {
     const int cb = clip_pel((int)(pred & 0xffffu) + (int)(int16_t)(res & 0xffffu), 255);
     const int cr = clip_pel((int)(pred >> 16) + ((int)res >> 16), 255);
     return (uint32_t)cb | (uint32_t)cr << 16;
+}
+
+// Fast Cb+Cr 8x8 pair (J5_FAST, component mask 3): as recon_fast, with Cb and Cr packed in the
+// 16-bit halves of each lane (cpred).  Lane k gathers reference sample Clip3(fa, la, k),
+// k = 0..32, of both components (the Cr copy of a neighbour sits 1024 B further in the CTU
+// interior, 32 B in the left column, cw B in the line buffer); lane l predicts sample
+// (l & 7, l >> 3) of both.  r32 = this lane's residual pair Cb | Cr << 16; line_cb = the row
+// above the CTU in the Cb line buffer.
+__device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, uint32_t cw, uint32_t w0, uint32_t w1,
+                                             uint32_t w5, int r32, int lane) {
+    constexpr int n = 8, ist = 32;
+    const int ofs = (int)(w0 & 0x1fffu);
+    const int xr = (ofs - 4096) & 31, yr = (ofs - 4096) >> 5;
+    const int mode = (int)((w0 >> 17) & 63u);
+    const int k = min(lane, 4 * n);
+    const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
+    const int sref = min(max(k, fa), la);
+    const uint32_t orgA = lbase + kOrgC + (uint32_t)ofs;                            // Cb TB origin
+    const uint32_t lcolA = lbase + (uint32_t)offsetof(WaveLds, cleft) + (uint32_t)yr;
+    const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
+    const int ls = xr == 0 ? 1 : ist;
+    const uint32_t tb = (yr == 0 ? line_cb + (uint32_t)xr : orgA - ist) - 2 * n - 1;
+    const int th = 2 * n + (yr > 0 ? 1 : 0);
+    const bool left = sref < th;
+    const uint32_t sa = tb + sref + (left ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
+    const uint32_t dcr = left ? (xr == 0 ? 32u : 1024u) : (yr == 0 ? cw : 1024u);
+    const uint32_t cb = *lds8(sa), cr = *lds8(sa + dcr);
+    const uint32_t v = (w0 & J_NONE) ? 0x00800080u : (cb | cr << 16);
+    const int x = lane & 7, y = lane >> 3;
+    const uint32_t rec = cquad_recon(cpred<3>(mode, w1, v, x, y, k), (uint32_t)r32);
+    const uint32_t da = orgA + (uint32_t)(y * ist + x);
+    *lds8(da) = (uint8_t)rec;
+    *lds8(da + 1024) = (uint8_t)(rec >> 16);
+    wave_sync();
 }
 
 // One stage of a 4x4 quad job (recon_quad): sub-TB Q of the 8x8 region.  Lane k of the
@@ -587,7 +645,7 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     }
     if constexpr (CH) {
         v = none ? 0x00800080 : v;
-        const uint32_t pred = cquad_pred(mode, angw, (uint32_t)v, xs, ys, lane);
+        const uint32_t pred = cpred<2>(mode, angw, (uint32_t)v, xs, ys, lane);
         return qid == Q ? (int)cquad_recon(pred, (uint32_t)r16) : rec;
     } else {
         v = none ? 128 : v;
@@ -611,7 +669,7 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     const int ofs = (int)(w0 & 0x1fffu);
     const int X = CH ? ((ofs - 4096) & 31) : (ofs & 63), Y = CH ? ((ofs - 4096) >> 5) : (ofs >> 6);
     const int half = CH ? (lane >> 5) : 0;
-    const uint32_t orgA = lbase + (uint32_t)ofs + (uint32_t)(half * 1024);
+    const uint32_t orgA = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)(half * 1024);
     const uint32_t leftA = lbase + (uint32_t)(CH ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft));
     // ---- external references: e = 0..12 column x = -1 (row e - 1), e = 13..24 row y = -1 ------
     const int e = min(CH ? (lane & 31) : lane, 24);
@@ -651,14 +709,20 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
         rec = quad_stage<3, CH>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
                                 ang(m), r16, qid, xs, ys);
     }
-    const uint32_t da = lbase + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
+    const uint32_t da = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
     *lds8(da) = (uint8_t)rec;
     if constexpr (CH) *lds8(da + 1024) = (uint8_t)(rec >> 16);
     wave_sync();
 }
 
-template <int W>
-__global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __restrict__ pics,
+// WPE = waves per SIMD the register allocation must allow (1: unconstrained).  W = 10 / 12 need
+// 5 / 6 for two workgroups per CU (at most 96 / 80 VGPRs).  W = 8 comes twice: unconstrained
+// (≈100 VGPRs) for a batch that runs alone, and register-lean (WPE 6: 80 VGPRs, a few spills)
+// for batches overlapping other batches' residual / loop-filter kernels, whose waves then
+// fit beside it on every SIMD (p265r.hip launch_rows; measured in DESIGN.md §6).
+template <int W, int WPE>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
+void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
                                                            const int16_t* __restrict__ resid,
                                                            Geo g, int n_pics, int fs_count, int lead,
@@ -683,7 +747,19 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
 
     // intraPredAngle | -invAngle << 8 of mode m in lane m (quad jobs read theirs with v_readlane)
     const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)c_angle[lane] | (uint32_t)(-(int)c_inv_angle[lane]) << 8) : 0;
-    if (threadIdx.x == 0) { ctl.next_row = 0; ctl.error = 0; }
+    if (threadIdx.x == 0) {
+        ctl.next_row = 0; ctl.error = 0;
+        ctl.cu_slot = -1; ctl.cu_rank = 0;
+        if (g.fair) {
+            uint32_t xcc, hwid;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+            const int key = (int)((xcc & 7u) * 128u + ((hwid >> 8) & 127u));      // CU_ID, SH_ID, SE_ID
+            RowCuSlot* cs = reinterpret_cast<RowCuSlot*>(err_flag + 64) + key;
+            ctl.cu_slot = key;
+            ctl.cu_rank = __hip_atomic_fetch_add(&cs->count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1;
+        }
+    }
     if (threadIdx.x < 32) ctl.done[threadIdx.x] = 0;
     for (int i = threadIdx.x; i < fs_count * units; i += 64 * W) prog[i] = -1;
     __syncthreads();
@@ -720,6 +796,16 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         r = __builtin_amdgcn_readfirstlane(r);
         if (r >= rows_total || failed) break;
         P265R_TRACE(2 | (r << 8));
+        if (g.fair) {
+            // publish the rows this workgroup has dequeued; priority 1 while behind the partner
+            const int key = __builtin_amdgcn_readfirstlane(ctl.cu_slot), rank = __builtin_amdgcn_readfirstlane(ctl.cu_rank);
+            RowCuSlot* cs = reinterpret_cast<RowCuSlot*>(err_flag + 64) + key;
+            if (lane == 0) __hip_atomic_store(&cs->prog[rank], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int other = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&cs->prog[rank ^ 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (r < other) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const int j = r / units, rem = r - j * units;
         // queue order inside a picture: the luma chain (the longer one) leads by `lead` rows:
         // L0 .. L(d-1), then L(d) C0 L(d+1) C1 ..., then the remaining chroma rows.  Either
@@ -776,6 +862,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
             // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr)
             const uint8_t* ltop_l = line_up + x0;
             const uint8_t* ltop_c = line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
+            const uint8_t* ltop_cb = line_up + g.w + (x0 >> 1);
 
             // residual of job t: two aligned 16-B loads per lane (fixed shape, pools padded
             // by 64 B), issued while job t-1 is processed.  TB offsets are multiples of 16.
@@ -828,6 +915,10 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                     const uint32_t w7 = (uint32_t)__builtin_amdgcn_readlane(rec1.w, l);
                     const uint32_t o = (lane & 32) ? ((lane & 4) ? w7 : w6) : ((lane & 4) ? j.w4 : j.w3);
                     r16n = *gptr(resid + (int)o + ((lane >> 1) & 12) + (lane & 3));
+                } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 15u) == 13u) { // Cb+Cr 8x8: Cb | Cr << 16 of sample lane
+                    const uint32_t cb = (uint16_t)*gptr(resid + (int)j.w3 + lane);
+                    const uint32_t cr = (uint16_t)*gptr(resid + (int)j.w4 + lane);
+                    r16n = (int)(cb | cr << 16);
                 } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) { // 16x16 luma: 4 samples per lane
                     const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(resid + (int)j.w3 + 4 * lane));
                     ra = make_uint4(d.x, d.y, 0u, 0u);
@@ -857,10 +948,11 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                 // (7 inlined instances would otherwise hold them all live: ~150 VGPRs).
                 int ln;
                 asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-                uint32_t lbase, tl, tc;
+                uint32_t lbase, tl, tc, tcb;
                 asm volatile("s_mov_b32 %0, %1" : "=s"(lbase) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&L)));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"((uint32_t)(uintptr_t)ltop_l));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tc) : "v"((uint32_t)(uintptr_t)ltop_c));
+                asm volatile("s_mov_b32 %0, %1" : "=s"(tcb) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ltop_cb)));
                 WaveLds& LL = *reinterpret_cast<WaveLds*>(lds_ptr(lbase));
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
@@ -872,6 +964,7 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
                         case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln); break;
                         case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln); break;
                         case 2: recon_fast16(lbase, tl, w0, w1, w5, ca, ln); break;
+                        case 5: recon_cfast8(lbase, tcb, (uint32_t)g.cw, w0, w1, w5, c16, ln); break;
                         default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln); break;
                     }
                 } else switch (sel) {
@@ -923,6 +1016,14 @@ __global__ __launch_bounds__(64 * W) void intra_rows_kernel(const DevPic* __rest
         const int slotw = gridDim.x * W + 2 * (blockIdx.x * W + wave);
         __hip_atomic_store(dbg + slotw, (int)(t_all >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(dbg + slotw + 1, (int)(t_wait >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (wave == 0) {            // placement of the workgroup: XCC id, HW_ID (CU / SE)
+            uint32_t xcc, hwid;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+            const int slotp = 3 * gridDim.x * W + 2 * blockIdx.x;
+            __hip_atomic_store(dbg + slotp, (int)xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(dbg + slotp + 1, (int)hwid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     // all stores of this wave are issued before it ends (compiler barrier)
     asm volatile("" ::: "memory");

@@ -86,7 +86,9 @@ struct p265r_ctx {
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
-    int row_waves = 8;         // waves per workgroup of the row pipeline (4, 8 or 16); 8 = 2 workgroups per CU
+    int row_waves = 8;         // waves per workgroup of the row pipeline (4, 6, 8, 10, 12, 16); 8 = 2 workgroups per CU
+    int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
+                               // while other lanes have work queued (P265R_LEAN)
     int luma_lead = 3;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
                                // measured, 1080p W=8: lead 0/1/2/3/5/8/17 -> 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
     int num_cus = 256;
@@ -107,7 +109,9 @@ struct p265r_ctx {
     // (ordered against the lane by events), so freed CU slots go to the long intra kernels first
     // (measured, 512 x 1080p: 3 lanes 12.10-12.15 -> 12.42-12.51 ms/step, 2 lanes 12.30 -> 12.01;
     // off by default)
-    bool prio = false;
+    // P265R_PRIO=2: one shared intra stream instead (normal priority): the intra kernels of
+    // all lanes run one after another while residual / loop-filter phases run beside them
+    int prio = 0;
     std::vector<hipStream_t> lanes_hi;
     std::vector<hipEvent_t> lane_ev;  // 2 per lane: residual phase done, intra phase done
 };
@@ -197,9 +201,10 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     return P265R_OK;
 }
 
-template <int W>
-int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
-    const Geo& g = ctx->geo;
+template <int W, int WPE>
+int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, bool alone) {
+    Geo g = ctx->geo;
+    g.fair = g.fair && alone;
     // picture slots: the W rows in flight are consecutive in the queue, so they span at
     // most ceil(W / hc) + 1 pictures; a slot is reused only after its previous picture is
     // complete (the kernel waits for that, so fewer slots would still be correct)
@@ -208,7 +213,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
         return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
-    auto fn = intra_rows_kernel<W>;
+    auto fn = intra_rows_kernel<W, WPE>;
     {
         // every workgroup resident at once and holding a single picture: one slot is enough
         // (a second picture would only wait for the first), and the smaller LDS footprint can
@@ -227,9 +232,9 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
     const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
     int* dbg = nullptr;
     if (ctx->debug_sync) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * grid * W * 3, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(dbg, 0, sizeof(int) * grid * W * 3);
-        fprintf(stderr, "[p265r] rows kernel W=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, grid, lds, fs, per_cu);
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * (grid * W * 3 + grid * 2), hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(dbg, 0, sizeof(int) * (grid * W * 3 + grid * 2));
+        fprintf(stderr, "[p265r] rows kernel W=%d WPE=%d fair=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, WPE, g.fair, grid, lds, fs, per_cu);
     }
     fn<<<grid, 64 * W, lds, b->intra_stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
     HIP_TRY(hipGetLastError());
@@ -248,18 +253,47 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b) {
         double tot = 0, wt = 0;
         for (int i = 0; i < grid * W; ++i) { tot += dbg[grid * W + 2 * i]; wt += dbg[grid * W + 2 * i + 1]; }
         fprintf(stderr, "[p265r] rows kernel: %.1f%% of wave time in dependency waits (%d waves)\n", 100.0 * wt / (tot > 0 ? tot : 1), grid * W);
+        // workgroup lifetimes (longest wave of each, 256-cycle units): the kernel ends with the slowest
+        std::vector<int> life(grid, 0);
+        for (int i = 0; i < grid * W; ++i) life[i / W] = std::max(life[i / W], dbg[grid * W + 2 * i]);
+        {   // by XCC and by CU slot: where do the slow workgroups run?
+            double sx[16] = {}; int nx[16] = {};
+            for (int i = 0; i < grid; ++i) { const int x = dbg[3 * grid * W + 2 * i] & 15; sx[x] += life[i]; ++nx[x]; }
+            fprintf(stderr, "[p265r] mean workgroup lifetime per XCC (Mcycles):");
+            for (int x = 0; x < 16; ++x) if (nx[x]) fprintf(stderr, " x%d:%.2f(%d)", x, sx[x] / nx[x] * 256e-6, nx[x]);
+            fprintf(stderr, "\n");
+            std::vector<std::pair<int, int>> byhw;
+            for (int i = 0; i < grid; ++i) byhw.push_back({dbg[3 * grid * W + 2 * i] * 128 + ((dbg[3 * grid * W + 2 * i + 1] >> 8) & 127), life[i]});
+            std::sort(byhw.begin(), byhw.end());
+            int same = 0; double dsum = 0;
+            for (size_t i = 1; i < byhw.size(); ++i)
+                if (byhw[i].first == byhw[i - 1].first) { ++same; dsum += std::abs(byhw[i].second - byhw[i - 1].second); }
+            fprintf(stderr, "[p265r] workgroups sharing a CU: %d pairs, mean lifetime difference %.2f Mcycles\n", same, same ? dsum / same * 256e-6 : 0.0);
+            for (int i = 0; i < 24 && i < grid; ++i)
+                fprintf(stderr, "  wg %d xcc %d hwid 0x%x life %.2f\n", i, dbg[3 * grid * W + 2 * i], dbg[3 * grid * W + 2 * i + 1], life[i] * 256e-6);
+        }
+        std::sort(life.begin(), life.end());
+        if (grid > 0)
+            fprintf(stderr, "[p265r] rows kernel workgroup lifetime (Mcycles): min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+                    life[0] * 256e-6, life[grid / 10] * 256e-6, life[grid / 2] * 256e-6, life[grid * 9 / 10] * 256e-6,
+                    life[grid - 1] * 256e-6);
         (void)hipHostFree(dbg);
     }
     return P265R_OK;
 }
 
-int launch_rows(p265r_ctx* ctx, p265r_batch* b) {
+// alone: no other lane of the context has work queued, so this batch's kernels have the GPU to
+// themselves (fair CU sharing, the unconstrained W = 8 build); otherwise the register-lean build
+int launch_rows(p265r_ctx* ctx, p265r_batch* b, bool alone) {
     switch (ctx->row_waves) {
-        case 4: return launch_rows_w<4>(ctx, b);
-        case 6: return launch_rows_w<6>(ctx, b);
-        case 10: return launch_rows_w<10>(ctx, b);
-        case 16: return launch_rows_w<16>(ctx, b);
-        default: return launch_rows_w<8>(ctx, b);
+        case 4: return launch_rows_w<4, 1>(ctx, b, alone);
+        case 6: return launch_rows_w<6, 1>(ctx, b, alone);
+        case 10: return launch_rows_w<10, 5>(ctx, b, alone);
+        case 12: return launch_rows_w<12, 6>(ctx, b, alone);
+        case 16: return launch_rows_w<16, 1>(ctx, b, alone);
+        default:
+            if (ctx->lean == 1 || (ctx->lean < 0 && !alone)) return launch_rows_w<8, 6>(ctx, b, alone);
+            return launch_rows_w<8, 1>(ctx, b, alone);
     }
 }
 
@@ -320,16 +354,19 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.nf_w = (g.w + 7) / 8;
     g.cqp[0] = p.pps_cb_qp_offset;
     g.cqp[1] = p.pps_cr_qp_offset;
+    g.fair = 1;
+    if (const char* v = std::getenv("P265R_FAIR")) g.fair = v[0] != '0';
     g.quad = 3;
-    if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 3;
+    if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 7;
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
-    if (const char* v = std::getenv("P265R_PRIO")) ctx->prio = v[0] == '1';
+    if (const char* v = std::getenv("P265R_PRIO")) ctx->prio = std::atoi(v) == 2 ? 2 : (v[0] == '1' ? 1 : 0);
+    if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
-        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 16) ctx->row_waves = w;
+        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 16) ctx->row_waves = w;
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -360,7 +397,8 @@ void p265r_destroy(p265r_ctx* ctx) {
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
     for (auto& e : ctx->spare) (void)hipEventDestroy(e);
     for (size_t i = 1; i < ctx->lanes.size(); ++i) (void)hipStreamDestroy(ctx->lanes[i]);
-    for (hipStream_t st : ctx->lanes_hi) (void)hipStreamDestroy(st);
+    for (size_t i = 0; i < ctx->lanes_hi.size(); ++i)                 // (P265R_PRIO=2: one stream, listed per lane)
+        if (i == 0 || ctx->lanes_hi[i] != ctx->lanes_hi[0]) (void)hipStreamDestroy(ctx->lanes_hi[i]);
     for (hipEvent_t ev : ctx->lane_ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
@@ -419,7 +457,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t pic_plane_bytes = align_up(plane_bytes[0], 256) + 2 * align_up(plane_bytes[1], 256);
     size_t off = 0;
     const size_t o_pics = off; off = align_up(off + sizeof(DevPic) * n_pics, 256);
-    const size_t o_err = off; off = align_up(off + 256, 256);
+    // error word (+ the row kernel's per-CU workgroup slots, kRowCuSlots x 16 B, intra_rows.h)
+    const size_t o_err = off; off = align_up(off + 256 + kRowCuSlots * 16, 256);
     const size_t o_ctus = off; off = align_up(off + sizeof(p265r_ctu) * nc * (size_t)n_pics, 256);
     const size_t o_tbs = off; off = align_up(off + sizeof(p265r_tb) * n_tbs_total, 256);
     // both pools padded by 64 B: the intra kernel reads fixed-shape 32-B runs
@@ -677,8 +716,15 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     b->intra_stream = s;
     if (recon && ctx->schedule == 1) {
-        HIP_TRY(hipMemsetAsync(b->d_err, 0, sizeof(int), s));
-        int rc = launch_rows(ctx, b);
+        HIP_TRY(hipMemsetAsync(b->d_err, 0, 256 + kRowCuSlots * 16, s));
+        // does another lane still have work queued (batches overlapping)?
+        bool alone = true;
+        for (size_t i = 0; i < ctx->lanes.size(); ++i)
+            if ((int)i != b->lane && hipStreamQuery(ctx->lanes[i]) != hipSuccess) alone = false;
+        for (size_t i = 0; i < ctx->lanes_hi.size(); ++i)
+            if (ctx->lanes_hi[i] != s && hipStreamQuery(ctx->lanes_hi[i]) != hipSuccess) alone = false;
+        (void)hipGetLastError();                    // hipStreamQuery's hipErrorNotReady is not an error
+        int rc = launch_rows(ctx, b, alone);
         if (rc) return rc;
         ++tm.intra_launches;
     }
@@ -820,7 +866,8 @@ int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         while ((int)ctx->lanes_hi.size() < depth) {
             hipStream_t st = nullptr;
-            HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+            if (ctx->prio == 2 && !ctx->lanes_hi.empty()) st = ctx->lanes_hi[0];
+            else HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, ctx->prio == 2 ? least : greatest));
             ctx->lanes_hi.push_back(st);
             for (int k = 0; k < 2; ++k) {
                 hipEvent_t ev = nullptr;

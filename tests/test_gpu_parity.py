@@ -41,16 +41,27 @@ def _check(recon_mod, params, pics, label=""):
     return outs
 
 
-@pytest.fixture(params=["rows", "steps", "rows16", "rows4", "rows_noquad"])
+# row pipeline variants: waves per workgroup; P265R_QUAD job merging (bit 0 luma 4x4 quads, bit 1
+# chroma 4x4 quads, bit 2 Cb+Cr 8x8 pairs on the general path instead of the fast one); the
+# register-lean W = 8 build (P265R_LEAN=1) and fair CU sharing off (P265R_FAIR=0)
+ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"},
+                "rows_lean": {"P265R_ROW_WAVES": "8", "P265R_LEAN": "1", "P265R_FAIR": "0"},
+                "rows10": {"P265R_ROW_WAVES": "10"}, "rows12": {"P265R_ROW_WAVES": "12"},
+                "rows16": {"P265R_ROW_WAVES": "16"}, "rows4": {"P265R_ROW_WAVES": "4", "P265R_QUAD": "1"},
+                "rows_noquad": {"P265R_ROW_WAVES": "8", "P265R_QUAD": "4"}}
+
+
+@pytest.fixture(params=["rows", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad"])
 def schedule(request, monkeypatch):
-    """Both intra schedules (CU-local row pipeline with 4/8/16 waves, with and without luma
-    4x4 quad jobs; per-diagonal launches)."""
+    """Both intra schedules (CU-local row pipeline with 4..16 waves, the register-lean build,
+    with and without the luma / chroma 4x4 quad jobs and the Cb+Cr 8x8 fast path; per-diagonal
+    launches)."""
     if request.param == "steps":
         monkeypatch.setenv("P265R_SCHEDULE", "steps")
     else:
         monkeypatch.setenv("P265R_SCHEDULE", "rows")
-        monkeypatch.setenv("P265R_ROW_WAVES", {"rows": "8", "rows16": "16", "rows4": "4", "rows_noquad": "8"}[request.param])
-        monkeypatch.setenv("P265R_QUAD", "0" if request.param == "rows_noquad" else "1")
+        for k, v in ROW_VARIANTS[request.param].items():
+            monkeypatch.setenv(k, v)
     return request.param
 
 
