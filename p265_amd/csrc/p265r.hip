@@ -87,6 +87,7 @@ struct p265r_ctx {
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
     int row_waves = 8;         // waves per workgroup of the row pipeline (4, 6, 8, 10, 12, 16); 8 = 2 workgroups per CU
+    int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
                                // while other lanes have work queued (P265R_LEAN)
     int luma_lead = 3;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
@@ -134,6 +135,7 @@ struct p265r_batch {
     bool sao = false;
     bool dbk = false;          // some CTU of the batch has deblocking on
     bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
+    int runs = 0;              // p265r_batch_run calls so far
 };
 
 namespace {
@@ -362,6 +364,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
     if (const char* v = std::getenv("P265R_PRIO")) ctx->prio = std::atoi(v) == 2 ? 2 : (v[0] == '1' ? 1 : 0);
+    if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
@@ -669,31 +672,36 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // ---- residual phase ----------------------------------------------------------
     const int bdl = g.bd[0], bdc = g.bd[1];
     const bool recon = !b->recon_input;
-    if (recon && b->n_jobs[RC_DST4]) {
+    // timing experiments only (P265R_SKIP bit 0: residual kernels, bit 1: job preparation, bit 2:
+    // loop filters) on RE-RUNS of a resident batch: its residuals / job lists from the previous
+    // run are still in place, so the output is unchanged while the skipped phase costs nothing
+    const int skip = b->runs > 0 ? ctx->skip : 0;
+    ++b->runs;
+    if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
         residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl);
         ++tm.residual_launches;
     }
-    if (recon && b->n_jobs[RC_DCT4]) {
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT4]) {
         residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc);
         ++tm.residual_launches;
     }
-    if (recon && b->n_jobs[RC_DCT8]) {
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT8]) {
         residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (recon && b->n_jobs[RC_DCT16]) {
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT16]) {
         residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (recon && b->n_jobs[RC_DCT32]) {
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT32]) {
         residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (recon && b->n_jobs[RC_TSKIP]) {
+    if (recon && !(skip & 1) && b->n_jobs[RC_TSKIP]) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (recon && ctx->schedule == 1) {
+    if (recon && ctx->schedule == 1 && !(skip & 2)) {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
         // of the residuals, timed with the residual phase
         intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
@@ -747,7 +755,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         s = s_lane;
     }
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
-    if (b->dbk || b->sao) {
+    if ((b->dbk || b->sao) && !(skip & 4)) {
         const long long units = (long long)ctx->n_ctus * b->n_pics;
         if (units >= (1ll << 31) - 8) return P265R_ERANGE;
         const dim3 grid((unsigned)((units + 7) / 8 * 8));
