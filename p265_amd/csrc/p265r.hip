@@ -27,6 +27,7 @@
 #include "loopfilter.h"
 #include "residual.h"
 #include "sao.h"
+#include "sao_rows.h"
 #include "tables.h"
 
 using namespace p265r;
@@ -87,6 +88,7 @@ struct p265r_ctx {
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
     int row_waves = 8;         // waves per workgroup of the row pipeline (4, 6, 8, 10, 12, 16); 8 = 2 workgroups per CU
+    bool sao_rows = true;      // SAO-only batches: streaming SAO kernel (P265R_SAO_ROWS=0: loop-filter kernel)
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
                                // while other lanes have work queued (P265R_LEAN)
@@ -364,6 +366,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
     if (const char* v = std::getenv("P265R_PRIO")) ctx->prio = std::atoi(v) == 2 ? 2 : (v[0] == '1' ? 1 : 0);
+    if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = v[0] != '0';
     if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
@@ -755,7 +758,16 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         s = s_lane;
     }
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
-    if ((b->dbk || b->sao) && !(skip & 4)) {
+    if (b->sao && !b->dbk && ctx->sao_rows && !(skip & 4)) {
+        // SAO only: the streaming SAO kernel (sao_rows.h), one wave per (picture, component, CTB
+        // row, 256-sample strip), 4 waves per block, blocks dealt XCD-aware
+        const long long waves = (long long)sao_rows_units(g) * b->n_pics;
+        if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
+        const long long blocks = (waves + 3) / 4;
+        sao_rows_kernel<<<(unsigned)((blocks + 7) / 8 * 8), 256, 0, s>>>(b->d_pics, g, b->n_pics);
+        ++tm.sao_launches;
+        HIP_TRY(hipGetLastError());
+    } else if ((b->dbk || b->sao) && !(skip & 4)) {
         const long long units = (long long)ctx->n_ctus * b->n_pics;
         if (units >= (1ll << 31) - 8) return P265R_ERANGE;
         const dim3 grid((unsigned)((units + 7) / 8 * 8));

@@ -48,14 +48,15 @@ ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"},
                 "rows_lean": {"P265R_ROW_WAVES": "8", "P265R_LEAN": "1", "P265R_FAIR": "0"},
                 "rows10": {"P265R_ROW_WAVES": "10"}, "rows12": {"P265R_ROW_WAVES": "12"},
                 "rows16": {"P265R_ROW_WAVES": "16"}, "rows4": {"P265R_ROW_WAVES": "4", "P265R_QUAD": "1"},
-                "rows_noquad": {"P265R_ROW_WAVES": "8", "P265R_QUAD": "4"}}
+                "rows_noquad": {"P265R_ROW_WAVES": "8", "P265R_QUAD": "4"},
+                "rows_lf": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "0"}}
 
 
-@pytest.fixture(params=["rows", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad"])
+@pytest.fixture(params=["rows", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad", "rows_lf"])
 def schedule(request, monkeypatch):
     """Both intra schedules (CU-local row pipeline with 4..16 waves, the register-lean build,
     with and without the luma / chroma 4x4 quad jobs and the Cb+Cr 8x8 fast path; per-diagonal
-    launches)."""
+    launches); SAO-only batches by the streaming SAO kernel or the loop-filter kernel."""
     if request.param == "steps":
         monkeypatch.setenv("P265R_SCHEDULE", "steps")
     else:
