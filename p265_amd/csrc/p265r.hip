@@ -87,7 +87,9 @@ struct p265r_ctx {
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
-    int row_waves = 8;         // waves per workgroup of the row pipeline (4, 6, 8, 10, 12, 16); 8 = 2 workgroups per CU
+    int row_waves = 0;         // waves per workgroup of the row pipeline (P265R_ROW_WAVES 4, 6, 8, 10, 12, 16);
+                               // 0 = by run: a batch alone 12 (6 per SIMD, 80 VGPRs: lowest latency),
+                               // overlapping other lanes' batches 8 register-lean (room beside it)
     bool sao_rows = true;      // SAO-only batches: streaming SAO kernel (P265R_SAO_ROWS=0: loop-filter kernel)
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
@@ -290,6 +292,9 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, bool alone) {
 // themselves (fair CU sharing, the unconstrained W = 8 build); otherwise the register-lean build
 int launch_rows(p265r_ctx* ctx, p265r_batch* b, bool alone) {
     switch (ctx->row_waves) {
+        case 0:
+            if (alone) return launch_rows_w<12, 6>(ctx, b, alone);
+            return launch_rows_w<8, 6>(ctx, b, alone);
         case 4: return launch_rows_w<4, 1>(ctx, b, alone);
         case 6: return launch_rows_w<6, 1>(ctx, b, alone);
         case 10: return launch_rows_w<10, 5>(ctx, b, alone);

@@ -44,7 +44,7 @@ def _check(recon_mod, params, pics, label=""):
 # row pipeline variants: waves per workgroup; P265R_QUAD job merging (bit 0 luma 4x4 quads, bit 1
 # chroma 4x4 quads, bit 2 Cb+Cr 8x8 pairs on the general path instead of the fast one); the
 # register-lean W = 8 build (P265R_LEAN=1) and fair CU sharing off (P265R_FAIR=0)
-ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"},
+ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
                 "rows_lean": {"P265R_ROW_WAVES": "8", "P265R_LEAN": "1", "P265R_FAIR": "0"},
                 "rows10": {"P265R_ROW_WAVES": "10"}, "rows12": {"P265R_ROW_WAVES": "12"},
                 "rows16": {"P265R_ROW_WAVES": "16"}, "rows4": {"P265R_ROW_WAVES": "4", "P265R_QUAD": "1"},
@@ -52,7 +52,7 @@ ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"},
                 "rows_lf": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "0"}}
 
 
-@pytest.fixture(params=["rows", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad", "rows_lf"])
+@pytest.fixture(params=["rows", "rows_auto", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad", "rows_lf"])
 def schedule(request, monkeypatch):
     """Both intra schedules (CU-local row pipeline with 4..16 waves, the register-lean build,
     with and without the luma / chroma 4x4 quad jobs and the Cb+Cr 8x8 fast path; per-diagonal
