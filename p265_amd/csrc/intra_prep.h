@@ -64,7 +64,10 @@ enum : uint32_t {
     J5_QUAD = 1u << 30,
 };
 
-struct LumaJobLds { uint32_t w0, w1, w2, w3, w5; };   // luma job words staged in LDS (w4 = zero_off)
+// job words staged in LDS: w1 (intraPredAngle, invAngle, availability bit 32) is rebuilt from the
+// mode at emission, bit 32 travels in w5 bit 16 (kJ5Bit32); luma w4 is always the zero block
+constexpr uint32_t kJ5Bit32 = 1u << 16;
+struct LumaJobLds { uint32_t w0, w2, w3, w5; };
 
 // the four jobs at slots s..s+3 are the fast 4x4 luma TBs of one 8x8 region, in z-order
 __device__ __forceinline__ bool quad_jobs(const LumaJobLds* j) {
@@ -100,7 +103,7 @@ __device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j) {
     return q;
 }
 
-struct ChromaJobLds { uint32_t w0, w1, w2, w3, w4, w5; };   // chroma job words staged in LDS
+struct ChromaJobLds { uint32_t w0, w2, w3, w4, w5; };
 
 // the four jobs at slots s..s+3 are fast Cb+Cr 4x4 pairs of one 8x8 chroma region, in z-order,
 // and their eight residuals are addressable as base + 16 * code (code <= 14; 15 = zero block):
@@ -169,11 +172,17 @@ __device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265
 // luma and chroma 4x4 quads can be merged before the lists are written, compacted.
 constexpr int kMaxCtuLuma = 256;
 constexpr int kMaxCtuChroma = 128;
-__device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_off) {
+__device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_off, uint32_t w1) {
     IntraJob J;
-    J.w[0] = l.w0; J.w[1] = l.w1; J.w[2] = l.w2; J.w[3] = l.w3;
-    J.w[4] = zero_off; J.w[5] = l.w5; J.w[6] = J.w[7] = 0;
+    J.w[0] = l.w0; J.w[1] = w1; J.w[2] = l.w2; J.w[3] = l.w3;
+    J.w[4] = zero_off; J.w[5] = l.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
     return J;
+}
+// job word w1 of a staged job: intraPredAngle | -invAngle << 8 (lane m of angtab holds mode m's),
+// availability bit 32 << 21.  ds_bpermute: call with every lane active.
+__device__ __forceinline__ uint32_t job_w1(int angtab, uint32_t w0, uint32_t w5) {
+    const int mode = (int)((w0 >> 17) & 63u);
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(mode << 2, angtab) | ((w5 & kJ5Bit32) ? 1u << 21 : 0u);
 }
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g) {
     __shared__ LumaJobLds sj[kMaxCtuLuma];
@@ -183,6 +192,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const DevPic P = pics[blockIdx.y];
     const int addr = blockIdx.x;
     const int lane = threadIdx.x;
+    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)(int8_t)kIntraPredAngle[lane] | (uint32_t)(-kInvAngle[lane]) << 8) : 0;
     const int cx = addr % g.wc, cy = addr / g.wc;
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
@@ -277,8 +287,9 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             }
             J.w[5] = w5;
             J.w[6] = J.w[7] = 0;
-            if (kl) sj[slot] = LumaJobLds{J.w[0], J.w[1], J.w[2], J.w[3], J.w[5]};
-            else if (slot < kMaxCtuChroma) sc[slot] = ChromaJobLds{J.w[0], J.w[1], J.w[2], J.w[3], J.w[4], J.w[5]};
+            const uint32_t w5s = J.w[5] | ((J.w[1] >> 21) & 1u ? kJ5Bit32 : 0u);
+            if (kl) sj[slot] = LumaJobLds{J.w[0], J.w[2], J.w[3], w5s};
+            else if (slot < kMaxCtuChroma) sc[slot] = ChromaJobLds{J.w[0], J.w[2], J.w[3], J.w[4], w5s};
         }
     }
     const int n_luma = out_l, n_chroma = min(out_c, kMaxCtuChroma);
@@ -301,15 +312,16 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const bool absorbed = valid && ((s >= 1 && chead[s - 1]) || (s >= 2 && chead[s - 2]) || (s >= 3 && chead[s - 3]));
         const bool emit = valid && !absorbed;
         const unsigned long long me_ = __ballot(emit);
+        const ChromaJobLds c = valid ? sc[s] : ChromaJobLds{0, 0, 0, 0, 0};
+        const uint32_t w1 = job_w1(angtab, c.w0, c.w5);
         if (emit) {
             IntraJob J;
             uint32_t qb = 0, qc = 0;
             if (chead[s] && cquad_jobs(sc + s, P.zero_off, qb, qc)) {
                 J = make_cquad(sc + s, qb, qc, P.zero_off);
             } else {
-                const ChromaJobLds& c = sc[s];
-                J.w[0] = c.w0; J.w[1] = c.w1; J.w[2] = c.w2; J.w[3] = c.w3;
-                J.w[4] = c.w4; J.w[5] = c.w5; J.w[6] = J.w[7] = 0;
+                J.w[0] = c.w0; J.w[1] = w1; J.w[2] = c.w2; J.w[3] = c.w3;
+                J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
             }
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + rank(me_));
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
@@ -324,8 +336,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const bool absorbed = valid && ((s >= 1 && head[s - 1]) || (s >= 2 && head[s - 2]) || (s >= 3 && head[s - 3]));
         const bool emit = valid && !absorbed;
         const unsigned long long me_ = __ballot(emit);
+        const LumaJobLds l = valid ? sj[s] : LumaJobLds{0, 0, 0, 0};
+        const uint32_t w1 = job_w1(angtab, l.w0, l.w5);
         if (emit) {
-            const IntraJob J = head[s] ? make_quad(sj + s) : luma_job(sj[s], P.zero_off);
+            const IntraJob J = head[s] ? make_quad(sj + s) : luma_job(l, P.zero_off, w1);
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + n_out + rank(me_));
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
