@@ -21,7 +21,10 @@
 
 namespace p265r {
 
-constexpr int kSaoRowsChunk = 8;           // output rows per load batch
+#ifndef P265R_SAO_CHUNK
+#define P265R_SAO_CHUNK 8
+#endif
+constexpr int kSaoRowsChunk = P265R_SAO_CHUNK;   // output rows per load batch
 
 constexpr int kSaoStrip = 248;             // output samples per strip (62 dwords)
 
