@@ -116,6 +116,9 @@ struct p265r_ctx {
     // off by default)
     // P265R_PRIO=2: one shared intra stream instead (normal priority): the intra kernels of
     // all lanes run one after another while residual / loop-filter phases run beside them
+    // P265R_PRIO=3: per lane a normal-priority twin runs intra + in-loop filters, so the lane
+    // starts the next batch's residual / prep phases while this batch's filters still run (the
+    // lane waits only for the previous run's intra kernel, which reads the residuals)
     int prio = 0;
     std::vector<hipStream_t> lanes_hi;
     std::vector<hipEvent_t> lane_ev;  // 2 per lane: residual phase done, intra phase done
@@ -140,6 +143,8 @@ struct p265r_batch {
     bool dbk = false;          // some CTU of the batch has deblocking on
     bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
     int runs = 0;              // p265r_batch_run calls so far
+    hipEvent_t intra_done = nullptr;  // P265R_PRIO=3: its last intra phase (on the twin stream)
+    bool intra_pending = false;
 };
 
 namespace {
@@ -370,7 +375,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
-    if (const char* v = std::getenv("P265R_PRIO")) ctx->prio = std::atoi(v) == 2 ? 2 : (v[0] == '1' ? 1 : 0);
+    if (const char* v = std::getenv("P265R_PRIO")) { const int pv = std::atoi(v); ctx->prio = pv >= 1 && pv <= 3 ? pv : 0; }
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = v[0] != '0';
     if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
@@ -669,6 +674,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     hipStream_t s = b->stream;
     const Geo& g = ctx->geo;
     p265r_timings tm{};
+    const bool twin_lf = b->stream_hi && ctx->prio == 3;   // filters stay on the twin (P265R_PRIO=3)
+    if (twin_lf && b->intra_pending) HIP_TRY(hipStreamWaitEvent(s, b->intra_done, 0));   // residuals free
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (ctx->timing) {
         for (auto& e : ev) {
@@ -757,7 +764,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     HIP_TRY(hipGetLastError());
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
-    if (s != s_lane) {                           // back to the lane: loop filters after the intra phase
+    if (twin_lf) {                               // filters follow on the twin; mark the residuals free
+        if (!b->intra_done) HIP_TRY(hipEventCreateWithFlags(&b->intra_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(b->intra_done, s));
+        b->intra_pending = true;
+    } else if (s != s_lane) {                    // back to the lane: loop filters after the intra phase
         HIP_TRY(hipEventRecord(ctx->lane_ev[2 * b->lane + 1], s));
         HIP_TRY(hipStreamWaitEvent(s_lane, ctx->lane_ev[2 * b->lane + 1], 0));
         s = s_lane;
@@ -831,6 +842,7 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     hipError_t e = hipSuccess;
     if (b->stream && b->stream != ctx->stream) e = hipStreamSynchronize(b->stream);   // its lane may still run it
     if (b->stream_hi && e == hipSuccess) e = hipStreamSynchronize(b->stream_hi);
+    if (b->intra_done) (void)hipEventDestroy(b->intra_done);
     if (b->mem) {
         // keep the larger of (cache, this allocation) for the next upload; callers free a batch
         // only once its work is complete (download/sync), and reuse is ordered on ctx->stream
@@ -892,7 +904,7 @@ int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
         while ((int)ctx->lanes_hi.size() < depth) {
             hipStream_t st = nullptr;
             if (ctx->prio == 2 && !ctx->lanes_hi.empty()) st = ctx->lanes_hi[0];
-            else HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, ctx->prio == 2 ? least : greatest));
+            else HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, ctx->prio == 1 ? greatest : least));
             ctx->lanes_hi.push_back(st);
             for (int k = 0; k < 2; ++k) {
                 hipEvent_t ev = nullptr;

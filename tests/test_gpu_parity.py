@@ -155,9 +155,12 @@ def test_resident_batch_rerun_is_stable(recon_mod):
             np.testing.assert_array_equal(first[i][c], second[i][c])
 
 
-def test_pipelined_batches(recon_mod):
+@pytest.mark.parametrize("prio", ["0", "1", "3"])
+def test_pipelined_batches(recon_mod, prio, monkeypatch):
     """p265r_set_pipeline: three resident batches on different streams, each run several times
-    back to back with the runs interleaved across streams, every output equals the oracle."""
+    back to back with the runs interleaved across streams, every output equals the oracle --
+    intra on the lane itself, on a high-priority twin, or intra + filters on a twin (P265R_PRIO)."""
+    monkeypatch.setenv("P265R_PRIO", prio)
     params = R.make_params(pic_width=320, pic_height=192)
     sets = [[synth.make_picture(params, 700 + 10 * k + s, perf=bool(s % 2)) for s in range(3)] for k in range(3)]
     pd = R.params_dict(params)
