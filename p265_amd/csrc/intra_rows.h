@@ -761,6 +761,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         }
     }
     if (threadIdx.x < 32) ctl.done[threadIdx.x] = 0;
+#ifdef P265R_JOB_STATS
+    if (threadIdx.x < 28) ctl.pad[threadIdx.x] = 0;
+#endif
     for (int i = threadIdx.x; i < fs_count * units; i += 64 * W) prog[i] = -1;
     __syncthreads();
 
@@ -932,6 +935,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             JobS cur{0, 0, 0, 0, 0, 0};
             if (nt) { refill(0); cur = sjob(0); issue(cur, 0); }
             for (int t = 0; t < nt; ++t) {
+#ifdef P265R_JOB_STATS
+                const long long tj0 = __builtin_amdgcn_s_memtime();
+#endif
                 // next job's record and residual are fetched before this job runs; this job
                 // works on copies of its own (measured: issuing after the job is slower)
                 const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w5 = cur.w5;
@@ -976,6 +982,17 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                     case 5: recon_job<3, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
                     default: recon_job<4, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
                 }
+#ifdef P265R_JOB_STATS
+                {   // per job class: cycles (/16) and count, summed in LDS (RowCtrl::pad), P265R_DEBUG_SYNC prints
+                    const int jc = (w5 & J5_QUAD) ? (((w0 >> 15) & 3u) ? 1 : 0)
+                                 : (w5 & J5_FAST) ? (sel == 5 ? 6 : (sel >= 4 ? 5 : 2 + sel)) : 7 + sel;
+                    const int dt = (int)((__builtin_amdgcn_s_memtime() - tj0) >> 4);
+                    if (lane == 0) {
+                        __hip_atomic_fetch_add(&ctl.pad[2 * jc], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&ctl.pad[2 * jc + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+#endif
             }
 
             P265R_TRACE(5 | (cx << 8) | (r << 16));
@@ -1011,6 +1028,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         P265R_TRACE(6 | (r << 8));
     }
     P265R_TRACE(7);
+#ifdef P265R_JOB_STATS
+    __syncthreads();
+    if (dbg && threadIdx.x < 28)
+        atomicAdd(dbg + 3 * gridDim.x * W + 2 * gridDim.x + threadIdx.x, ctl.pad[threadIdx.x]);
+#endif
     if (dbg) {   // debug statistics: [total cycles, cycles in dependency waits] per wave
         const long long t_all = __builtin_amdgcn_s_memtime() - t_begin;
         const int slotw = gridDim.x * W + 2 * (blockIdx.x * W + wave);

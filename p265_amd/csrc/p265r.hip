@@ -243,8 +243,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, bool alone) {
     const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
     int* dbg = nullptr;
     if (ctx->debug_sync) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * (grid * W * 3 + grid * 2), hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(dbg, 0, sizeof(int) * (grid * W * 3 + grid * 2));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * (grid * W * 3 + grid * 2 + 32), hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(dbg, 0, sizeof(int) * (grid * W * 3 + grid * 2 + 32));
         fprintf(stderr, "[p265r] rows kernel W=%d WPE=%d fair=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, WPE, g.fair, grid, lds, fs, per_cu);
     }
     fn<<<grid, 64 * W, lds, b->intra_stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
@@ -282,6 +282,17 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, bool alone) {
             fprintf(stderr, "[p265r] workgroups sharing a CU: %d pairs, mean lifetime difference %.2f Mcycles\n", same, same ? dsum / same * 256e-6 : 0.0);
             for (int i = 0; i < 24 && i < grid; ++i)
                 fprintf(stderr, "  wg %d xcc %d hwid 0x%x life %.2f\n", i, dbg[3 * grid * W + 2 * i], dbg[3 * grid * W + 2 * i + 1], life[i] * 256e-6);
+        }
+        {   // per job class (P265R_JOB_STATS builds): jobs, cycles per job
+            static const char* names[14] = {"luma quad", "chroma quad", "fast Y4", "fast Y8", "fast Y16", "fast C4 pair",
+                                            "fast C8 pair", "gen Y4", "gen Y8", "gen Y16", "gen Y32", "gen C4", "gen C8", "gen C16"};
+            const int* js = dbg + 3 * grid * W + 2 * grid;
+            double tot = 0;
+            for (int k = 0; k < 14; ++k) tot += 16.0 * (unsigned)js[2 * k];
+            for (int k = 0; k < 14; ++k)
+                if (js[2 * k + 1])
+                    fprintf(stderr, "[p265r] jobs %-13s %9d  %7.0f cycles/job  %5.1f %%\n", names[k], js[2 * k + 1],
+                            16.0 * (unsigned)js[2 * k] / js[2 * k + 1], 100.0 * 16.0 * (unsigned)js[2 * k] / (tot > 0 ? tot : 1));
         }
         std::sort(life.begin(), life.end());
         if (grid > 0)
