@@ -76,6 +76,15 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ lds_u8* lds8(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
 __device__ __forceinline__ lds_u32* lds32(uint32_t a) { return (lds_u32*)(uintptr_t)a; }
 
+// Signed 24-bit product (both |operands| < 2^23): the projected-reference index r * invAngle
+// (8.4.4.2.6), which LLVM otherwise widens to a quarter-rate v_mul_lo_u32 once it knows both
+// factors are negative
+__device__ __forceinline__ int mul_i24(int a, int b) {
+    int r;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 struct WaveLds {                 // one wave's private CTU state (4432 B): a wave holds one row
     uint8_t  ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
     union {                      // ref: raw / final linear reference arrays (8-bit samples)
@@ -213,15 +222,12 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                 if (!all) {
                     const int u = k < 2 * n ? (k >> US) : (k == 2 * n ? NU : NU + 1 + ((k - 2 * n - 1) >> US));
                     const unsigned long long below = m & ((1ull << u) - 1ull);
-                    if (!((m >> u) & 1ull)) {
-                        if (below) {
-                            const int ub = 63 - __clzll((long long)below);        // nearest available unit below
-                            s = ub < NU ? (ub << US) + (1 << US) - 1 : (ub == NU ? 2 * n : 2 * n + ((ub - NU) << US));
-                        } else {
-                            const int uf = __ffsll((long long)m) - 1;             // first available unit
-                            s = uf < NU ? (uf << US) : (uf == NU ? 2 * n : 2 * n + 1 + ((uf - NU - 1) << US));
-                        }
-                    }
+                    // both substitution candidates computed, then selected (no divergent branch)
+                    const int ub = 63 - __clzll((long long)(below | 1ull));   // nearest available unit below
+                    const int sb = ub < NU ? (ub << US) + (1 << US) - 1 : (ub == NU ? 2 * n : 2 * n + ((ub - NU) << US));
+                    const int uf = __ffsll((long long)m) - 1;                 // first available unit
+                    const int sf = uf < NU ? (uf << US) : (uf == NU ? 2 * n : 2 * n + 1 + ((uf - NU - 1) << US));
+                    s = ((m >> u) & 1ull) ? k : (below ? sb : sf);
                 }
                 const uint8_t* src = s < 2 * n ? lbase + (2 * n - 1 - s) * lstep : (s == 2 * n ? cptr : tbase + (s - 2 * n - 1));
                 const int v = none ? 128 : (int)*src;
@@ -286,19 +292,19 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
             const int inv = -(int)((w1 >> 8) & 0x1fffu);
             if (mode >= 18) {                                        // vertical family
                 const int idx = ((sy + 1) * ang) >> 5, fact = ((sy + 1) * ang) & 31;
-                auto refk = [&](int r) { return r >= 0 ? 2 * n + r : 2 * n - ((r * inv + 128) >> 8); };
+                auto refk = [&](int r) { const int p = mul_i24(r, inv); return r >= 0 ? 2 * n + r : 2 * n - ((p + 128) >> 8); };
                 const bool bflt = !PAIR && n < 32 && mode == 26;
 #pragma unroll
                 for (int i = 0; i < S; ++i) {
                     const int x = sx + i;
                     const int r0 = x + idx + 1;
                     int v = R[refk(r0)];
-                    if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
+                    v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;   // fact = 0: v
                     if (bflt && x == 0) v = clip_pel((int)R[2 * n + 1] + (((int)R[2 * n - 1 - sy] - (int)R[2 * n]) >> 1), maxv);
                     put(i, v);
                 }
             } else {                                                 // horizontal family
-                auto refk = [&](int r) { return r >= 0 ? 2 * n - r : 2 * n + ((r * inv + 128) >> 8); };
+                auto refk = [&](int r) { const int p = mul_i24(r, inv); return r >= 0 ? 2 * n - r : 2 * n + ((p + 128) >> 8); };
                 const bool bflt = !PAIR && n < 32 && mode == 10 && sy == 0;
 #pragma unroll
                 for (int i = 0; i < S; ++i) {
@@ -306,7 +312,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                     const int idx = ((x + 1) * ang) >> 5, fact = ((x + 1) * ang) & 31;
                     const int r0 = sy + idx + 1;
                     int v = R[refk(r0)];
-                    if (fact) v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;
+                    v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;   // fact = 0: v
                     if (bflt) v = clip_pel((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), maxv);
                     put(i, v);
                 }
@@ -366,7 +372,7 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
         const int idx = pa >> 5, fact = pa & 31;
         const int r0 = across + idx + 1;
         auto refk = [&](int r) {                                 // r < 0: projected side reference (invAngle)
-            const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
+            const int p = mul_i24(r, inv), t = r >= 0 ? r : -((p + 128) >> 8);
             return vert ? 2 * n + t : 2 * n - t;
         };
         const bool bflt = !PAIR && (mode == 26 || mode == 10);
@@ -498,7 +504,7 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
         const int ang = (int)(int8_t)(w1 & 0xffu);
         const int inv = -(int)((w1 >> 8) & 0x1fffu);
         auto refk = [&](int r, bool vert) {
-            const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
+            const int p = mul_i24(r, inv), t = r >= 0 ? r : -((p + 128) >> 8);
             return vert ? 2 * n + t : 2 * n - t;
         };
         if (mode >= 18) {                                     // vertical: one projection row per lane
@@ -571,7 +577,7 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
     const int idx = pa >> 5, fact = pa & 31;
     const int r0 = across + idx + 1;
     auto refk = [&](int r) {
-        const int t = r >= 0 ? r : -((__mul24(r, inv) + 128) >> 8);
+        const int p = mul_i24(r, inv), t = r >= 0 ? r : -((p + 128) >> 8);
         return vert ? 2 * n + t : 2 * n - t;
     };
     const uint32_t a = ref(refk(r0)), b = ref(refk(r0 + 1));
@@ -645,12 +651,12 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     }
     if constexpr (CH) {
         v = none ? 0x00800080 : v;
-        const uint32_t pred = cpred<2>(mode, angw, (uint32_t)v, xs, ys, lane);
-        return qid == Q ? (int)cquad_recon(pred, (uint32_t)r16) : rec;
+        const int rq = (int)cquad_recon(cpred<2>(mode, angw, (uint32_t)v, xs, ys, lane), (uint32_t)r16);
+        return qid == Q ? rq : rec;
     } else {
         v = none ? 128 : v;
-        const int pred = fast_pred<2, false>(mode, angw, v, xs, ys, lane, lane, 0);
-        return qid == Q ? clip_pel(pred + r16, maxv) : rec;
+        const int rq = clip_pel(fast_pred<2, false>(mode, angw, v, xs, ys, lane, lane, 0) + r16, maxv);
+        return qid == Q ? rq : rec;
     }
 }
 
@@ -673,16 +679,12 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     const uint32_t leftA = lbase + (uint32_t)(CH ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft));
     // ---- external references: e = 0..12 column x = -1 (row e - 1), e = 13..24 row y = -1 ------
     const int e = min(CH ? (lane & 31) : lane, 24);
-    uint32_t ea;
-    if (e <= 12) {
-        const int r = min(Y - 1 + e, last);                      // rows below the CTU: never available
-        const uint32_t in_left = X > 0 ? orgA - 1 + (uint32_t)((e - 1) * ist) : leftA + (uint32_t)r;
-        ea = r < 0 ? line_top + (uint32_t)(X - 1)
-                   : (X > 0 && Y - 1 + e > last ? orgA - (uint32_t)(Y * ist) + (uint32_t)(last * ist) - 1 : in_left);
-    } else {
-        const int c = e - 13;
-        ea = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - ist + (uint32_t)min(c, last - X);
-    }
+    // every candidate computed, then selected: no divergent branch per lane class
+    const int r = min(Y - 1 + e, last);                          // rows below the CTU: never available
+    const int c = e - 13;
+    const uint32_t col = X > 0 ? orgA - 1 + (uint32_t)((r - Y) * ist) : leftA + (uint32_t)r;
+    const uint32_t row = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - ist + (uint32_t)min(c, last - X);
+    const uint32_t ea = e > 12 ? row : (r < 0 ? line_top + (uint32_t)(X - 1) : col);
     int ext = (int)*lds8(ea);
     if constexpr (CH) ext |= __builtin_amdgcn_ds_bpermute(((lane + 32) & 63) << 2, ext) << 16;   // Cb | Cr << 16
     const int xs = lane & 3, ys = (lane >> 3) & 3;
@@ -1009,11 +1011,14 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int ist = c ? 32 : 64;
                 P265R_GLOBAL uint8_t* plane = gptr_w(uniform(gload(&Pp->rec[c])));
                 const int st = g.stride[c];
-                const int gpr = wv >> 2;
-                for (int e = lane; e < gpr * hv; e += 64) {
-                    const int yy = e / gpr, xx = (e - yy * gpr) << 2;
-                    *reinterpret_cast<P265R_GLOBAL uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
-                        *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
+                // 2^lg words (4 samples) per CTB row, no per-word division; the words past a
+                // picture's right edge idle
+                const int lg = g.ctb_log2 - sub - 2;
+                for (int e = lane; e < (hv << lg); e += 64) {
+                    const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << 2;
+                    if (xx < wv)
+                        *reinterpret_cast<P265R_GLOBAL uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
+                            *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
                 }
                 unsigned char* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
                 if (lane < wv) lc[lane] = src[(hv - 1) * ist + lane];
