@@ -78,11 +78,31 @@ __device__ __forceinline__ lds_u32* lds32(uint32_t a) { return (lds_u32*)(uintpt
 
 // Signed 24-bit product (both |operands| < 2^23): the projected-reference index r * invAngle
 // (8.4.4.2.6), which LLVM otherwise widens to a quarter-rate v_mul_lo_u32 once it knows both
-// factors are negative
+// factors are negative.  b is wave-uniform (invAngle of the job's mode) and goes in an SGPR.
 __device__ __forceinline__ int mul_i24(int a, int b) {
     int r;
-    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "s"(b), "v"(a));
     return r;
+}
+
+// Angular reference index (8.4.4.2.6) in the linear order of 8.4.4.2.2 (left column reversed at
+// 0..2n-1, corner 2n, top row 2n+1..4n) of projection position r:
+//   idx = 2n + s * (r >= 0 ? r : -((r * invAngle + 128) >> 8)),  s = +1 vertical, -1 horizontal.
+// With nr = -r and ia = |invAngle| (>= 256 for every negative intraPredAngle; 256 stands in for
+// the modes without one, ang_inv), the bracket equals -max(nr, (nr * ia + 128) >> 8) for EVERY r
+// (r >= 0: the product rounds to <= -r; r < 0: it rounds to >= |r|), so the index needs no
+// per-lane select on the sign of r: idx = 2n + ns * max(...), ns = -s (wave-uniform).
+template <int TWO_N>
+__device__ __forceinline__ int ang_ref(int nr, int ia, int ns) {
+    const int q = (mul_i24(nr, ia) + 128) >> 8;
+    int r;   // TWO_N + ns * max(nr, q) in one v_mad_i32_i24 (LLVM widens ns * x to v_mul_lo_u32: |ns| = 1)
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "s"(ns), "v"(max(nr, q)), "i"(TWO_N));
+    return r;
+}
+// |invAngle| of job word w1 / angtab bits [8,21), 256 for the modes without an inverse angle
+__device__ __forceinline__ int ang_inv(uint32_t angw) {
+    const int ia = (int)((angw >> 8) & 0x1fffu);
+    return ia ? ia : 256;
 }
 
 struct WaveLds {                 // one wave's private CTU state (4432 B): a wave holds one row
@@ -133,16 +153,24 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ int clip_pel(int v, int maxv) { return min(max(v, 0), maxv); }
 
-// sum of v over the 32-lane half of the wave (PAIR) or the whole wave
-template <bool PAIR>
+// sum of v over the 32-lane half of the wave (PAIR) or the whole wave; NR = how many 16-lane
+// rows from the start of each half can hold non-zero values (1, 2 or 4: fewer lane reads)
+template <bool PAIR, int NR = 4>
 __device__ __forceinline__ int wave_sum(int v, int half) {
     v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
     v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);   // row_half_mirror
     v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true);   // row_mirror: every lane holds its row's sum
-    const int s0 = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);
-    const int s1 = __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
-    return PAIR ? (half ? s1 : s0) : s0 + s1;
+    auto rl = [&](int l) { return __builtin_amdgcn_readlane(v, l); };
+    if constexpr (NR == 1) {
+        return PAIR ? (half ? rl(32) : rl(0)) : rl(0);
+    } else if constexpr (NR == 2) {
+        return PAIR ? (half ? rl(32) + rl(48) : rl(0) + rl(16)) : rl(0) + rl(16);
+    } else {
+        const int s0 = rl(0) + rl(16);
+        const int s1 = rl(32) + rl(48);
+        return PAIR ? (half ? s1 : s0) : s0 + s1;
+    }
 }
 
 // Reconstruct one intra job of size 2^LOG2: a luma TB (PAIR = false, 64 lanes) or the
@@ -289,10 +317,10 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
             }
         } else {
             const int ang = (int)(int8_t)(w1 & 0xffu);
-            const int inv = -(int)((w1 >> 8) & 0x1fffu);
+            const int ia = ang_inv(w1);
             if (mode >= 18) {                                        // vertical family
                 const int idx = ((sy + 1) * ang) >> 5, fact = ((sy + 1) * ang) & 31;
-                auto refk = [&](int r) { const int p = mul_i24(r, inv); return r >= 0 ? 2 * n + r : 2 * n - ((p + 128) >> 8); };
+                auto refk = [&](int r) { return ang_ref<2 * n>(-r, ia, -1); };
                 const bool bflt = !PAIR && n < 32 && mode == 26;
 #pragma unroll
                 for (int i = 0; i < S; ++i) {
@@ -304,7 +332,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                     put(i, v);
                 }
             } else {                                                 // horizontal family
-                auto refk = [&](int r) { const int p = mul_i24(r, inv); return r >= 0 ? 2 * n - r : 2 * n + ((p + 128) >> 8); };
+                auto refk = [&](int r) { return ang_ref<2 * n>(-r, ia, 1); };
                 const bool bflt = !PAIR && n < 32 && mode == 10 && sy == 0;
 #pragma unroll
                 for (int i = 0; i < S; ++i) {
@@ -354,7 +382,7 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
                 __mul24(y + 1, uref(n - 1)) + n) >> (LOG2 + 1);
     } else if (mode == 1) {
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
-        const int dc = (wave_sum<PAIR>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
+        const int dc = (wave_sum<PAIR, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
         if (PAIR) {
             pred = dc;
         } else {                                                 // luma n < 32: edge smoothing
@@ -365,19 +393,17 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
         }
     } else {
         const int ang = (int)(int8_t)(angw & 0xffu);
-        const int inv = -(int)((angw >> 8) & 0x1fffu);
+        const int ia = ang_inv(angw);
         const bool vert = mode >= 18;
+        const int ns = vert ? -1 : 1;
         const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
         const int pa = __mul24(along + 1, ang);
         const int idx = pa >> 5, fact = pa & 31;
-        const int r0 = across + idx + 1;
-        auto refk = [&](int r) {                                 // r < 0: projected side reference (invAngle)
-            const int p = mul_i24(r, inv), t = r >= 0 ? r : -((p + 128) >> 8);
-            return vert ? 2 * n + t : 2 * n - t;
-        };
+        const int nr0 = -1 - across - idx;                       // -(iIdx + across + 1)
         const bool bflt = !PAIR && (mode == 26 || mode == 10);
-        const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : refk(r0 + 1);
-        const int a = ref(refk(r0)), b = ref(i1);
+        const int k1 = ang_ref<2 * n>(nr0 - 1, ia, ns);          // computed unconditionally: a select, no branch
+        const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : k1;
+        const int a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(i1);
         pred = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;   // = a when iFact = 0 (b then unused)
         if (bflt) {                                              // modes 26 / 10, luma: boundary smoothing
             const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
@@ -502,11 +528,8 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
         }
     } else {
         const int ang = (int)(int8_t)(w1 & 0xffu);
-        const int inv = -(int)((w1 >> 8) & 0x1fffu);
-        auto refk = [&](int r, bool vert) {
-            const int p = mul_i24(r, inv), t = r >= 0 ? r : -((p + 128) >> 8);
-            return vert ? 2 * n + t : 2 * n - t;
-        };
+        const int ia = ang_inv(w1);
+        auto refk = [&](int r, bool vert) { return ang_ref<2 * n>(-r, ia, vert ? -1 : 1); };
         if (mode >= 18) {                                     // vertical: one projection row per lane
             const int pa = __mul24(y + 1, ang);
             const int idx = pa >> 5, fact = pa & 31;
@@ -528,7 +551,8 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
                 const int idx = pa >> 5, fact = pa & 31;
                 const int r0 = y + idx + 1;
                 const int a = ref(refk(r0, false));
-                const int b = ref(mode == 10 ? 2 * n + 1 + x : refk(r0 + 1, false));
+                const int k1 = refk(r0 + 1, false);
+                const int b = ref(mode == 10 ? 2 * n + 1 + x : k1);
                 pred[i] = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;
                 if (mode == 10) pred[i] = y == 0 ? clip_pel(left0 + ((b - corner) >> 1), maxv) : pred[i];
             }
@@ -566,21 +590,18 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
     }
     if (mode == 1) {
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
-        const uint32_t s = (uint32_t)wave_sum<false>(in ? (int)v : 0, 0) + rnd;
+        const uint32_t s = (uint32_t)wave_sum<false, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>(in ? (int)v : 0, 0) + rnd;
         return (s >> (LOG2 + 1)) & msk;
     }
     const int ang = (int)(int8_t)(angw & 0xffu);
-    const int inv = -(int)((angw >> 8) & 0x1fffu);
+    const int ia = ang_inv(angw);
     const bool vert = mode >= 18;
+    const int ns = vert ? -1 : 1;
     const int along = vert ? y : x, across = vert ? x : y;
     const int pa = __mul24(along + 1, ang);
     const int idx = pa >> 5, fact = pa & 31;
-    const int r0 = across + idx + 1;
-    auto refk = [&](int r) {
-        const int p = mul_i24(r, inv), t = r >= 0 ? r : -((p + 128) >> 8);
-        return vert ? 2 * n + t : 2 * n - t;
-    };
-    const uint32_t a = ref(refk(r0)), b = ref(refk(r0 + 1));
+    const int nr0 = -1 - across - idx;
+    const uint32_t a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(ang_ref<2 * n>(nr0 - 1, ia, ns));
     return ((__umul24(32 - fact, a) + __umul24(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
 }
 
