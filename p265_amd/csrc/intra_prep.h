@@ -172,6 +172,7 @@ __device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265
 // luma and chroma 4x4 quads can be merged before the lists are written, compacted.
 constexpr int kMaxCtuLuma = 256;
 constexpr int kMaxCtuChroma = 128;
+constexpr int kPrepChunks = (kMaxCtuLuma + kMaxCtuChroma + 63) / 64;   // TB records per CTU / 64
 __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_off, uint32_t w1) {
     IntraJob J;
     J.w[0] = l.w0; J.w[1] = w1; J.w[2] = l.w2; J.w[3] = l.w3;
@@ -213,13 +214,44 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     auto rank = [&](unsigned long long m) {
         return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     };
-    for (int base = 0; base < cnt; base += 64) {
+    // every TB record of the CTU is loaded up front, one 16-B load per lane and chunk, all in
+    // flight together (tb_count <= 384 at CTB 64, validate_picture); a TB's predecessor and
+    // successor come from the neighbouring lanes (DPP wave shifts, chunk edges by v_readlane)
+    uint4 rv[kPrepChunks];
+    const uint4* tv = reinterpret_cast<const uint4*>(tbs);
+#pragma unroll
+    for (int i = 0; i < kPrepChunks; ++i) {
+        const int t = i * 64 + lane;
+        rv[i] = t < cnt ? tv[t] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    auto from_prev_lane = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false); };
+    auto from_next_lane = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false); };
+    auto as_tb = [](uint4 v) { p265r_tb r; __builtin_memcpy(&r, &v, sizeof(r)); return r; };
+#pragma unroll
+    for (int ci = 0; ci < kPrepChunks; ++ci) {
+        const int base = ci * 64;
+        if (base >= cnt) break;                                   // wave-uniform
         const int t = base + lane;
         const bool valid = t < cnt;
+        const uint4 cv = rv[ci];
+        // words 0, 1 (position, size, component, mode, flags) of t - 1; words 0, 1, 3 of t + 1
+        uint4 pv = make_uint4(from_prev_lane(cv.x), from_prev_lane(cv.y), 0u, 0u);
+        uint4 nv = make_uint4(from_next_lane(cv.x), from_next_lane(cv.y), 0u, from_next_lane(cv.w));
+        if (ci > 0 && lane == 0) {
+            pv.x = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci - 1].x, 63);
+            pv.y = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci - 1].y, 63);
+        }
+        if (ci == 0 && lane == 0) pv = make_uint4(0u, 0u, 0u, 0u);
+        if (ci + 1 < kPrepChunks && lane == 63) {
+            nv.x = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci + 1].x, 0);
+            nv.y = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci + 1].y, 0);
+            nv.w = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci + 1].w, 0);
+        }
+        if (ci + 1 == kPrepChunks && lane == 63) nv = make_uint4(0u, 0u, 0u, 0u);
         p265r_tb rec{}, prev{}, next{};
-        if (valid) rec = tbs[t];
-        if (valid && t > 0) prev = tbs[t - 1];
-        if (valid && t + 1 < cnt) next = tbs[t + 1];
+        if (valid) rec = as_tb(cv);
+        if (valid && t > 0) prev = as_tb(pv);
+        if (valid && t + 1 < cnt) next = as_tb(nv);
         const bool cr_taken = valid && t > 0 && tb_same_tu_chroma(prev, rec);
         const bool keep = valid && !cr_taken;
         const bool kl = keep && rec.c_idx == 0;
