@@ -56,8 +56,8 @@ def measured_traffic(kernel_prefix, frames, avg_ms=None):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=512, help="1080p pictures per GPU per step")
     ap.add_argument("--unique", type=int, default=4, help="distinct synthetic pictures per rank (replicated)")
     ap.add_argument("--pipeline", type=int, default=3,

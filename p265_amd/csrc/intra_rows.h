@@ -29,6 +29,11 @@
 
 namespace p265r {
 
+// intraPredAngle 0 (modes 10 / 26) as plain copies in the fast paths (0 = the generic angular code)
+#ifndef P265R_HV_FAST
+#define P265R_HV_FAST 1
+#endif
+
 #define P265R_GLOBAL __attribute__((address_space(1)))
 template <typename T>
 __device__ __forceinline__ const P265R_GLOBAL T* gptr(const T* p) { return (const P265R_GLOBAL T*)p; }
@@ -391,6 +396,16 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
             const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
             pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
         }
+    } else if (P265R_HV_FAST && (angw & 0xffu) == 0u) {
+        // modes 10 / 26 (intraPredAngle 0): a copy of the column left / the row above, plus the
+        // luma boundary smoothing of 8.4.4.2.6 (fast jobs are n < 32) - no projection arithmetic
+        const bool vert = mode >= 18;
+        pred = ref(vert ? 2 * n + 1 + x : 2 * n - 1 - y);
+        if (!PAIR) {
+            const int b = ref(vert ? 2 * n - 1 - y : 2 * n + 1 + x);
+            const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
+            pred = (vert ? x : y) == 0 ? edge : pred;
+        }
     } else {
         const int ang = (int)(int8_t)(angw & 0xffu);
         const int ia = ang_inv(angw);
@@ -526,6 +541,20 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
             const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
             pred[i] = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
         }
+    } else if (P265R_HV_FAST && (w1 & 0xffu) == 0u) {        // modes 10 / 26: copies + boundary smoothing
+        if (mode >= 18) {
+            const int e = clip_pel(uref(2 * n + 1) + ((ref(2 * n - 1 - y) - uref(2 * n)) >> 1), maxv);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pred[i] = ref(2 * n + 1 + x0 + i);
+            pred[0] = x0 == 0 ? e : pred[0];
+        } else {
+            const int l = ref(2 * n - 1 - y), corner = uref(2 * n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int t = ref(2 * n + 1 + x0 + i);          // every lane: ds_bpermute outside any branch
+                pred[i] = y == 0 ? clip_pel(l + ((t - corner) >> 1), maxv) : l;
+            }
+        }
     } else {
         const int ang = (int)(int8_t)(w1 & 0xffu);
         const int ia = ang_inv(w1);
@@ -593,6 +622,8 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
         const uint32_t s = (uint32_t)wave_sum<false, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>(in ? (int)v : 0, 0) + rnd;
         return (s >> (LOG2 + 1)) & msk;
     }
+    if (P265R_HV_FAST && (angw & 0xffu) == 0u)                  // modes 10 / 26: a copy (no chroma smoothing)
+        return ref(mode >= 18 ? 2 * n + 1 + x : 2 * n - 1 - y);
     const int ang = (int)(int8_t)(angw & 0xffu);
     const int ia = ang_inv(angw);
     const bool vert = mode >= 18;
