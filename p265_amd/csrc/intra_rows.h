@@ -29,6 +29,11 @@
 
 namespace p265r {
 
+// s_sleep argument between two polls of a row-kernel dependency wait
+#ifndef P265R_SPIN_SLEEP
+#define P265R_SPIN_SLEEP 4
+#endif
+
 // intraPredAngle 0 (modes 10 / 26) as plain copies in the fast paths (0 = the generic angular code)
 #ifndef P265R_HV_FAST
 #define P265R_HV_FAST 1
@@ -837,7 +842,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             if (__builtin_amdgcn_readfirstlane((int)ready())) { t_wait += __builtin_amdgcn_s_memtime() - t0; return true; }
             if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 return false;
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(P265R_SPIN_SLEEP);   // 64 cycles per unit; each poll costs issue slots
         }
         __hip_atomic_store(&ctl.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // all lanes, same value
         atomicOr(err_flag, 1);
@@ -953,9 +958,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane(v, l); };
                 return JobS{rl(rec0.x), rl(rec0.y), rl(rec0.z), rl(rec0.w), rl(rec1.x), rl(rec1.y)};
             };
-            uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-            int r16n = 0;
-            auto issue = [&](const JobS& j, int ji) {           // residual loads of job j (index ji)
+            // prefetched residual of the next job: one sample per lane (fast / quad jobs; chroma: a
+            // Cb | Cr << 16 pair) in rn.x, a 16x16 job's four samples in rn.  General jobs
+            // (32x32 luma, 16x16 chroma, PCM, non-contiguous availability: ~2 % of the jobs) load their
+            // own 32 B per lane when they start: prefetching them too kept eight more VGPRs live
+            // across the loop and cost ~10 register copies per job
+            u32x2_t rn = {0u, 0u};
+            auto issue = [&](const JobS& j, int ji) -> u32x2_t {   // residual loads of job j (index ji)
                 if ((j.w5 & J5_QUAD) && ((j.w0 >> 15) & 3u)) {              // chroma quad: Cb | Cr << 16 of (x, y)
                     const int l = ji & 63;
                     const int zero = __builtin_amdgcn_readlane(rec1.z, l);      // w6 = zero_off
@@ -965,42 +974,39 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                     auto at = [&](uint32_t code) { return (code == 15u ? zero : (int)j.w3 + (int)(code << 4)) + i; };
                     const uint32_t cb = (uint16_t)*gptr(resid + at(codes & 15u));
                     const uint32_t cr = (uint16_t)*gptr(resid + at((codes >> 4) & 15u));
-                    r16n = (int)(cb | cr << 16);
+                    return u32x2_t{cb, cr};     // packed at use: no wait here
                 } else if (j.w5 & J5_QUAD) {                                // 4x4 quad: sample (x, y) of the 8x8 region
                     const int l = ji & 63;
                     const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane(rec1.z, l);
                     const uint32_t w7 = (uint32_t)__builtin_amdgcn_readlane(rec1.w, l);
                     const uint32_t o = (lane & 32) ? ((lane & 4) ? w7 : w6) : ((lane & 4) ? j.w4 : j.w3);
-                    r16n = *gptr(resid + (int)o + ((lane >> 1) & 12) + (lane & 3));
+                    return u32x2_t{(uint32_t)(int)*gptr(resid + (int)o + ((lane >> 1) & 12) + (lane & 3)), 0u};
                 } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 15u) == 13u) { // Cb+Cr 8x8: Cb | Cr << 16 of sample lane
                     const uint32_t cb = (uint16_t)*gptr(resid + (int)j.w3 + lane);
                     const uint32_t cr = (uint16_t)*gptr(resid + (int)j.w4 + lane);
-                    r16n = (int)(cb | cr << 16);
+                    return u32x2_t{cb, cr};     // packed at use: no wait here
                 } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) { // 16x16 luma: 4 samples per lane
                     const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(resid + (int)j.w3 + 4 * lane));
-                    ra = make_uint4(d.x, d.y, 0u, 0u);
+                    return d;
                 } else if (j.w5 & J5_FAST) {
-                    r16n = *gptr(res_fast(j.w0, j.w3, j.w4));
-                } else {
-                    const uint4* a = res_addr(j.w0, j.w3, j.w4);
-                    ra = ld16(a); rb = ld16(a + 1);
+                    return u32x2_t{(uint32_t)(int)*gptr(res_fast(j.w0, j.w3, j.w4)), 0u};
                 }
+                return u32x2_t{0u, 0u};
             };
             JobS cur{0, 0, 0, 0, 0, 0};
-            if (nt) { refill(0); cur = sjob(0); issue(cur, 0); }
+            if (nt) { refill(0); cur = sjob(0); rn = issue(cur, 0); }
             for (int t = 0; t < nt; ++t) {
 #ifdef P265R_JOB_STATS
                 const long long tj0 = __builtin_amdgcn_s_memtime();
 #endif
                 // next job's record and residual are fetched before this job runs; this job
                 // works on copies of its own (measured: issuing after the job is slower)
-                const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w5 = cur.w5;
-                const uint4 ca = ra, cb = rb;
-                const int c16 = r16n;
+                const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w3 = cur.w3, w4 = cur.w4, w5 = cur.w5;
+                const int c16 = (int)rn.x, c16m = (int)rn.y;
                 if (t + 1 < nt) {
                     if (((t + 1) & 63) == 0) refill(t + 1);
                     cur = sjob(t + 1);
-                    issue(cur, t + 1);
+                    rn = issue(cur, t + 1);
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
                 // Opaque copies of the lane id and the LDS bases: keeps the compiler from
@@ -1017,17 +1023,20 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_QUAD) {
-                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tc, w0, w1, w2, angtab, c16, ln);
+                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tc, w0, w1, w2, angtab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
                     else recon_quad<false>(lbase, tl, w0, w1, w2, angtab, c16, ln);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
                         case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln); break;
                         case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln); break;
-                        case 2: recon_fast16(lbase, tl, w0, w1, w5, ca, ln); break;
-                        case 5: recon_cfast8(lbase, tcb, (uint32_t)g.cw, w0, w1, w5, c16, ln); break;
+                        case 2: recon_fast16(lbase, tl, w0, w1, w5, make_uint4((uint32_t)c16, (uint32_t)c16m, 0u, 0u), ln); break;
+                        case 5: recon_cfast8(lbase, tcb, (uint32_t)g.cw, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln); break;
                         default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln); break;
                     }
-                } else switch (sel) {
+                } else {
+                  const uint4* ra_p = res_addr(w0, w3, w4);
+                  const uint4 ca = ld16(ra_p), cb = ld16(ra_p + 1);
+                  switch (sel) {
                     case 0: recon_job<2, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
                     case 1: recon_job<3, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
                     case 2: recon_job<4, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
@@ -1035,6 +1044,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                     case 4: recon_job<2, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
                     case 5: recon_job<3, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
                     default: recon_job<4, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
+                  }
                 }
 #ifdef P265R_JOB_STATS
                 {   // per job class: cycles (/16) and count, summed in LDS (RowCtrl::pad), P265R_DEBUG_SYNC prints
@@ -1063,14 +1073,28 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int ist = c ? 32 : 64;
                 P265R_GLOBAL uint8_t* plane = gptr_w(uniform(gload(&Pp->rec[c])));
                 const int st = g.stride[c];
-                // 2^lg words (4 samples) per CTB row, no per-word division; the words past a
-                // picture's right edge idle
-                const int lg = g.ctb_log2 - sub - 2;
-                for (int e = lane; e < (hv << lg); e += 64) {
-                    const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << 2;
-                    if (xx < wv)
-                        *reinterpret_cast<P265R_GLOBAL uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
-                            *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
+                if (cs >= 16) {
+                    // 2^lg 16-sample chunks per CTB row (one ds_read_b128 + one 16-B global store per
+                    // lane and chunk).  A chunk that straddles the picture's right edge is stored whole:
+                    // the plane rows are padded to 64 B (stride >= xb + cs), and nothing reads the
+                    // padding (downloads copy the width, SAO / deblocking clamp to it)
+                    const int lg = g.ctb_log2 - sub - 4;
+                    for (int e = lane; e < (hv << lg); e += 64) {
+                        const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << 4;
+                        if (xx < wv)
+                            *reinterpret_cast<P265R_GLOBAL u32x4_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
+                                *reinterpret_cast<const u32x4_t*>(src + yy * ist + xx);
+                    }
+                } else {
+                    // 2^lg words (4 samples) per CTB row, no per-word division; the words past a
+                    // picture's right edge idle
+                    const int lg = g.ctb_log2 - sub - 2;
+                    for (int e = lane; e < (hv << lg); e += 64) {
+                        const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << 2;
+                        if (xx < wv)
+                            *reinterpret_cast<P265R_GLOBAL uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
+                                *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
+                    }
                 }
                 unsigned char* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
                 if (lane < wv) lc[lane] = src[(hv - 1) * ist + lane];
