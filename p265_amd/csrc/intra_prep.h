@@ -28,7 +28,7 @@ namespace p265r {
 //      23 PCM  [24,26) filter (0 none, 1 [1 2 1], 2 strong candidate)
 //      [26,28) residual in the coefficient pool (bypass/PCM) per half
 //      [28,30) coded (residual non-zero) per half   30 all refs available   31 none available
-//  w1: [0,8) intraPredAngle (int8)  [8,21) -invAngle  21 availability bit 32
+//  w1: [0,8) intraPredAngle (int8)  [8,21) |invAngle| (256 for the modes without one)  21 availability bit 32
 //  w2: availability bits 0..31 (unit u: k in [u*us, u*us+us) for u < L, corner u = L,
 //      top units u > L; us = 4 luma / 2 chroma samples, L = 2N/us)
 //  w3, w4: residual element offset of half 0 (luma / Cb) and half 1 (Cr), int32 relative to
@@ -179,7 +179,7 @@ __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_
     J.w[4] = zero_off; J.w[5] = l.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
     return J;
 }
-// job word w1 of a staged job: intraPredAngle | -invAngle << 8 (lane m of angtab holds mode m's),
+// job word w1 of a staged job: intraPredAngle | |invAngle| << 8 (lane m of angtab holds mode m's; 256 without one),
 // availability bit 32 << 21.  ds_bpermute: call with every lane active.
 __device__ __forceinline__ uint32_t job_w1(int angtab, uint32_t w0, uint32_t w5) {
     const int mode = (int)((w0 >> 17) & 63u);
@@ -193,7 +193,9 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const DevPic P = pics[blockIdx.y];
     const int addr = blockIdx.x;
     const int lane = threadIdx.x;
-    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)(int8_t)kIntraPredAngle[lane] | (uint32_t)(-kInvAngle[lane]) << 8) : 0;
+    // intraPredAngle | |invAngle| << 8 per mode (256 for the modes without an inverse angle: intra_rows.h ang_inv)
+    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)(int8_t)kIntraPredAngle[lane] |
+                                         (uint32_t)(kInvAngle[lane] ? -kInvAngle[lane] : 256) << 8) : 0;
     const int cx = addr % g.wc, cy = addr / g.wc;
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;

@@ -111,8 +111,7 @@ __device__ __forceinline__ int ang_ref(int nr, int ia, int ns) {
 }
 // |invAngle| of job word w1 / angtab bits [8,21), 256 for the modes without an inverse angle
 __device__ __forceinline__ int ang_inv(uint32_t angw) {
-    const int ia = (int)((angw >> 8) & 0x1fffu);
-    return ia ? ia : 256;
+    return (int)((angw >> 8) & 0x1fffu);      // the angle tables store 256 for the modes without one
 }
 
 struct WaveLds {                 // one wave's private CTU state (4432 B): a wave holds one row
@@ -370,7 +369,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 
 // Prediction (8.4.4.2.4-6) of sample (x, y) of a fast job: lane k of v holds reference
 // sample k of this lane's half (linear order of 8.4.4.2.2, substituted, filtered);
-// angw = intraPredAngle (int8, bits 0..7) | -invAngle << 8 (job word w1's layout).
+// angw = intraPredAngle (int8, bits 0..7) | |invAngle| << 8 (job word w1's layout; 256 without one).
 template <int LOG2, bool PAIR>
 __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, int y, int k, int hl, int half) {
     constexpr int n = 1 << LOG2;
@@ -420,7 +419,7 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
         const int pa = __mul24(along + 1, ang);
         const int idx = pa >> 5, fact = pa & 31;
         const int nr0 = -1 - across - idx;                       // -(iIdx + across + 1)
-        const bool bflt = !PAIR && (mode == 26 || mode == 10);
+        const bool bflt = !P265R_HV_FAST && !PAIR && (mode == 26 || mode == 10);   // HV_FAST: copies above
         const int k1 = ang_ref<2 * n>(nr0 - 1, ia, ns);          // computed unconditionally: a select, no branch
         const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : k1;
         const int a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(i1);
@@ -572,7 +571,7 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
             for (int m = 0; m < 5; ++m) q[m] = ref(refk(x0 + idx + 1 + m, true));
 #pragma unroll
             for (int i = 0; i < 4; ++i) pred[i] = (__mul24(32 - fact, q[i]) + __mul24(fact, q[i + 1]) + 16) >> 5;
-            if (mode == 26) {                                 // x == 0: boundary smoothing
+            if (!P265R_HV_FAST && mode == 26) {               // x == 0: boundary smoothing (HV_FAST: above)
                 const int e = clip_pel(uref(2 * n + 1) + ((ref(2 * n - 1 - y) - uref(2 * n)) >> 1), maxv);
                 pred[0] = x0 == 0 ? e : pred[0];
             }
@@ -586,9 +585,9 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
                 const int r0 = y + idx + 1;
                 const int a = ref(refk(r0, false));
                 const int k1 = refk(r0 + 1, false);
-                const int b = ref(mode == 10 ? 2 * n + 1 + x : k1);
+                const int b = ref((!P265R_HV_FAST && mode == 10) ? 2 * n + 1 + x : k1);
                 pred[i] = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;
-                if (mode == 10) pred[i] = y == 0 ? clip_pel(left0 + ((b - corner) >> 1), maxv) : pred[i];
+                if (!P265R_HV_FAST && mode == 10) pred[i] = y == 0 ? clip_pel(left0 + ((b - corner) >> 1), maxv) : pred[i];
             }
         }
     }
@@ -804,8 +803,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
     unsigned char* lines = smem + 256 + prog_bytes + W * sizeof(WaveLds);
 
-    // intraPredAngle | -invAngle << 8 of mode m in lane m (quad jobs read theirs with v_readlane)
-    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)c_angle[lane] | (uint32_t)(-(int)c_inv_angle[lane]) << 8) : 0;
+    // intraPredAngle | |invAngle| << 8 (256 without one) of mode m in lane m (quad jobs read theirs with v_readlane)
+    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)c_angle[lane] | (uint32_t)(c_inv_angle[lane] ? -(int)c_inv_angle[lane] : 256) << 8) : 0;
     if (threadIdx.x == 0) {
         ctl.next_row = 0; ctl.error = 0;
         ctl.cu_slot = -1; ctl.cu_rank = 0;
