@@ -53,6 +53,35 @@ def measured_traffic(kernel_prefix, frames, avg_ms=None):
     return int(row["traffic_gb"] * 1e9), "%s, %s" % (tag, name.replace("void ", ""))
 
 
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32 at 2.4 GHz; a wave64 VALU op takes its SIMD 2 cycles;
+# one scalar unit per CU (1 SALU instruction per cycle)
+VALU_PEAK = 1024 * 2.4e9 / 2.0      # wave-instructions / s
+SALU_PEAK = 256 * 2.4e9             # instructions / s
+
+
+def issue_rates(kernel_prefix, avg_ms):
+    """Instruction-issue view of the dominant kernel (it is issue-bound): VALU and
+    SALU instructions per launch from the committed PMC summary (SQ_INSTS_VALU / SQ_INSTS_SALU of
+    the profiled build whose duration matches), divided by this run's launch time and the peaks."""
+    try:
+        tag = open(PROFILE).read().strip()
+        summ = json.load(open(os.path.join(ROOT, "profiles", tag, "summary.json")))
+    except (OSError, ValueError):
+        return None
+    rows = [(n, r) for n, r in summ.items() if kernel_prefix in n and r.get("SQ_INSTS_VALU") and r.get("isolated_dispatches")]
+    if not rows:
+        return None
+    name, row = min(rows, key=lambda nr: abs(nr[1]["avg_ms"] - avg_ms))
+    if abs(row["avg_ms"] - avg_ms) > 0.1 * avg_ms:
+        return None
+    t = avg_ms * 1e-3
+    return {"valu_per_launch": int(row["SQ_INSTS_VALU"]), "salu_per_launch": int(row["SQ_INSTS_SALU"]),
+            "valu_frac": round(row["SQ_INSTS_VALU"] / (t * VALU_PEAK), 3),
+            "salu_frac": round(row["SQ_INSTS_SALU"] / (t * SALU_PEAK), 3),
+            "source": "profiles/%s/summary.json, %s" % (tag, name.replace("void ", "")),
+            "peaks": "VALU 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 op; SALU 256 CUs x 2.4 GHz"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -245,7 +274,9 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": ("profiles/%s/summary.json (rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)" % prof_tag) if traffic else prof_tag,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
-                     "note": "latency/issue-bound dependency chain; see DESIGN.md §4 and profiles/"},
+                     "note": "instruction-issue-bound (VALU + the CU's one scalar unit), not HBM-bound: see "
+                             "issue_rates and DESIGN.md §4"},
+        "issue_rates": issue_rates("intra_rows_kernel", avg_launch_ms),
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
         "phase_gbs": {"residual": round(res_b / (acc["residual_ms"] / a.steps * 1e-3) / 1e9, 1),
                       "sao": round(sao_b / (acc["sao_ms"] / a.steps * 1e-3) / 1e9, 1) if acc["sao_ms"] else None,
