@@ -272,7 +272,8 @@ def main():
                    "parallelism": "picture-sharded x%d" % world},
         "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": ("profiles/%s/summary.json (rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)" % prof_tag) if traffic else prof_tag,
+                     "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
+                                        % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
                      "note": "instruction-issue-bound (VALU + the CU's one scalar unit), not HBM-bound: see "
                              "issue_rates and DESIGN.md §4"},
