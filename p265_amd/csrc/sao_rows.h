@@ -14,6 +14,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "../../include/p265r.h"
 #include "intra.h"
 #include "loopfilter.h"
@@ -34,7 +35,7 @@ __host__ __device__ __forceinline__ int sao_rows_units(const Geo& g) {
 }
 
 // grid: 4 waves per block, one wave per (picture, component, CTB row, strip), XCD-aware order
-__global__ __launch_bounds__(256) void sao_rows_kernel(const DevPic* __restrict__ pics, Geo g, int n_pics) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void sao_rows_kernel(const DevPic* __restrict__ pics, Geo g, int n_pics) {
     const int lane = threadIdx.x & 63;
     const int per_pic = sao_rows_units(g);
     const int total = per_pic * n_pics;
@@ -161,52 +162,62 @@ __global__ __launch_bounds__(256) void sao_rows_kernel(const DevPic* __restrict_
     // rows y0 - 1 .. y0 + K of the current chunk; the next chunk's K new rows are loaded before
     // the current chunk is filtered.  A chunk is one basic block (rows past the CTB row are
     // computed and not stored), so the scheduler interleaves its independent rows.
-    uint32_t rowv[K + 2], nxt[K];
-    rowv[0] = row_ld(yb - 1);
-    rowv[1] = row_ld(yb);
+    // waves without a band-offset CTB (about half of them: ~82 % of CTBs are edge-offset) skip the
+    // band arithmetic; the choice is wave-uniform
+    auto filter_rows = [&](auto has_bo) {
+        constexpr bool HB = decltype(has_bo)::value;
+        uint32_t rowv[K + 2], nxt[K];
+        rowv[0] = row_ld(yb - 1);
+        rowv[1] = row_ld(yb);
 #pragma unroll
-    for (int k = 2; k < K + 2; ++k) rowv[k] = row_ld(yb + k - 1);
-    for (int y0 = yb; y0 < ye; y0 += K) {
-        if (y0 + K < ye) {
+        for (int k = 2; k < K + 2; ++k) rowv[k] = row_ld(yb + k - 1);
+        for (int y0 = yb; y0 < ye; y0 += K) {
+            if (y0 + K < ye) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) nxt[k] = row_ld(y0 + K + k + 1);
+                for (int k = 0; k < K; ++k) nxt[k] = row_ld(y0 + K + k + 1);
+            }
+            uint32_t nfm[K];                                          // PCM / bypass samples: unchanged
+#pragma unroll
+            for (int k = 0; k < K; ++k) nfm[k] = 0u;
+            if (nf) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    nfm[k] = nf[(size_t)((min(y0 + k, H - 1) << sub) >> 3) * g.nf_w + ((Xc << sub) >> 3)] ? 0xffffffffu : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int y = y0 + k;
+                const uint32_t cur = rowv[k + 1], up = rowv[k], dn = rowv[k + 2];
+                const uint32_t lc = left_of(cur), rc = right_of(cur);
+                const uint32_t lu = left_of(up), ru_ = right_of(up);
+                const uint32_t ld = left_of(dn), rd_ = right_of(dn);
+                // edge offset: neighbours a, b of the 4 samples (byte-aligned) per SaoEoClass
+                const uint32_t a = (__builtin_amdgcn_alignbyte(cur, lc, 3) & mc0) | (up & mc1) |
+                                   (__builtin_amdgcn_alignbyte(up, lu, 3) & mc2) | (__builtin_amdgcn_alignbyte(ru_, up, 1) & mc3);
+                const uint32_t b = (__builtin_amdgcn_alignbyte(rc, cur, 1) & mc0) | (dn & mc1) |
+                                   (__builtin_amdgcn_alignbyte(rd_, dn, 1) & mc2) | (__builtin_amdgcn_alignbyte(dn, ld, 3) & mc3);
+                const uint32_t sel_eo = join(edge(split_lo(cur), split_lo(a), split_lo(b)), edge(split_hi(cur), split_hi(a), split_hi(b)));
+                uint32_t sel = sel_eo;
+                if constexpr (HB) {
+                    // band offset: slot 1..4 for the four bands from sao_band_position, else 0
+                    const uint32_t kk = (((cur >> 3) & 0x1f1f1f1fu) + badd) & 0x1f1f1f1fu;
+                    const uint32_t big = (((kk & 0x1c1c1c1cu) + 0x7f7f7f7fu) & 0x80808080u) >> 7;
+                    const uint32_t sel_bo = (kk + 0x01010101u) & ~((big << 8) - big);
+                    sel = (sel_eo & meo) | (sel_bo & ~meo);
+                }
+                // row kind (wave-uniform): picture's first / last row, CTB's first / last row, other
+                const uint32_t okm = ((y == 0 || y + 1 == H) ? ok_nv : (y == yb ? ok_top : (y == yb + cs - 1 ? ok_bot : ok_mid))) & ~nfm[k];
+                const uint32_t res = (apply(cur, sel) & okm) | (cur & ~okm);
+                if (act && y < ye) *(gu32*)(dst + (size_t)y * st + X) = res;
+            }
+            rowv[0] = rowv[K];
+            rowv[1] = rowv[K + 1];
+#pragma unroll
+            for (int k = 0; k < K; ++k) rowv[k + 2] = nxt[k];
         }
-        uint32_t nfm[K];                                          // PCM / bypass samples: unchanged
-#pragma unroll
-        for (int k = 0; k < K; ++k) nfm[k] = 0u;
-        if (nf) {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                nfm[k] = nf[(size_t)((min(y0 + k, H - 1) << sub) >> 3) * g.nf_w + ((Xc << sub) >> 3)] ? 0xffffffffu : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int y = y0 + k;
-            const uint32_t cur = rowv[k + 1], up = rowv[k], dn = rowv[k + 2];
-            const uint32_t lc = left_of(cur), rc = right_of(cur);
-            const uint32_t lu = left_of(up), ru_ = right_of(up);
-            const uint32_t ld = left_of(dn), rd_ = right_of(dn);
-            // edge offset: neighbours a, b of the 4 samples (byte-aligned) per SaoEoClass
-            const uint32_t a = (__builtin_amdgcn_alignbyte(cur, lc, 3) & mc0) | (up & mc1) |
-                               (__builtin_amdgcn_alignbyte(up, lu, 3) & mc2) | (__builtin_amdgcn_alignbyte(ru_, up, 1) & mc3);
-            const uint32_t b = (__builtin_amdgcn_alignbyte(rc, cur, 1) & mc0) | (dn & mc1) |
-                               (__builtin_amdgcn_alignbyte(rd_, dn, 1) & mc2) | (__builtin_amdgcn_alignbyte(dn, ld, 3) & mc3);
-            const uint32_t sel_eo = join(edge(split_lo(cur), split_lo(a), split_lo(b)), edge(split_hi(cur), split_hi(a), split_hi(b)));
-            // band offset: slot 1..4 for the four bands from sao_band_position, else 0
-            const uint32_t kk = (((cur >> 3) & 0x1f1f1f1fu) + badd) & 0x1f1f1f1fu;
-            const uint32_t big = (((kk & 0x1c1c1c1cu) + 0x7f7f7f7fu) & 0x80808080u) >> 7;
-            const uint32_t sel_bo = (kk + 0x01010101u) & ~((big << 8) - big);
-            const uint32_t sel = (sel_eo & meo) | (sel_bo & ~meo);
-            // row kind (wave-uniform): picture's first / last row, CTB's first / last row, other
-            const uint32_t okm = ((y == 0 || y + 1 == H) ? ok_nv : (y == yb ? ok_top : (y == yb + cs - 1 ? ok_bot : ok_mid))) & ~nfm[k];
-            const uint32_t res = (apply(cur, sel) & okm) | (cur & ~okm);
-            if (act && y < ye) *(gu32*)(dst + (size_t)y * st + X) = res;
-        }
-        rowv[0] = rowv[K];
-        rowv[1] = rowv[K + 1];
-#pragma unroll
-        for (int k = 0; k < K; ++k) rowv[k + 2] = nxt[k];
-    }
+    };
+    if (__ballot(act && typ == 1)) filter_rows(std::integral_constant<bool, true>{});
+    else filter_rows(std::integral_constant<bool, false>{});
 }
 
 }  // namespace p265r
