@@ -31,7 +31,7 @@ namespace p265r {
 
 // s_sleep argument between two polls of a row-kernel dependency wait
 #ifndef P265R_SPIN_SLEEP
-#define P265R_SPIN_SLEEP 4
+#define P265R_SPIN_SLEEP 8
 #endif
 
 // intraPredAngle 0 (modes 10 / 26) as plain copies in the fast paths (0 = the generic angular code)

@@ -94,7 +94,7 @@ struct p265r_ctx {
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
                                // while other lanes have work queued (P265R_LEAN)
-    int luma_lead = 3;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
+    int luma_lead = 5;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
                                // measured, 1080p W=8: lead 0/1/2/3/5/8/17 -> 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
