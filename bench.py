@@ -1,20 +1,31 @@
 #!/usr/bin/env python3
-"""Benchmark: reconstructed 1080p all-intra CTUs/s on MI355X (BASELINE.json metric).
+"""Benchmark: reconstructed all-intra CTUs/s on MI355X (BASELINE.json metric).
 
 A "step" is one pass of the hot path -- residual (dequant + inverse DCT/DST) -> intra
-prediction + reconstruction -> SAO -- over one batch of synthetic 1080p all-intra
-pictures whose records are already resident in HBM (config C3 shape with SAO on, i.e.
-C4's per-GPU work).  N GPUs: one process per GPU (torch.distributed.run); each rank
-decodes its own batch of independent pictures (weak scaling, no data-path collective);
-the 32-byte SPS/PPS POD is broadcast from rank 0 over RCCL once, outside the timed
-region.  Rank 0 prints ONE JSON line.
+prediction + reconstruction -> SAO -- over one batch of synthetic all-intra pictures whose
+records are already resident in HBM.
+
+  --workload c3  (default)  C3/C4: 1080p + SAO, 512 pictures per GPU per step (C4's per-GPU
+                            work: pictures are independent, picture f -> rank f mod N)
+  --workload c5             C5: 4K, 2x2 tiles x 2 frames = 8 tile units per step across all
+                            ranks ((frame, tile) -> rank, dist.unit_shard), CTU-row SAO
+
+N GPUs: one process per GPU (torch.distributed.run only launches them; nothing here imports
+torch).  Weak scaling for c3, no data-path collective; the 32-byte SPS/PPS POD is broadcast
+from rank 0 with ncclBroadcast (RCCL over xGMI, ctypes, p265_amd/rccl.py) once, outside the
+timed region; barriers and the MAX over ranks go over the socket control plane.  Rank 0
+prints ONE JSON line.
 
     python bench.py                       # N=1, defaults finish in ~1-2 minutes
-    torchrun --nproc-per-node 8 bench.py --gpus 8
+    python -m torch.distributed.run --nproc-per-node 8 bench.py --gpus 8
+
+P265R_* environment variables are experiment / test knobs of the library; bench refuses to run
+with any of them set unless --experiment is given (and then records them in the line).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -23,31 +34,39 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "reconstructed CTUs/sec (1080p all-intra) + achieved HBM GB/s vs peak"
-# rocprofv3 PMC summary of this same command (tools/profile_round.sh + tools/profile_summary.py);
-# its HBM traffic per intra launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction) fills roofline.traffic
-PROFILE = os.path.join(ROOT, "profiles", "LATEST")
+# rocprofv3 PMC summary of this same command per workload (tools/profile_round.sh +
+# tools/profile_summary.py); its HBM traffic per intra launch (2*FETCH_SIZE + WRITE_SIZE,
+# gfx950 correction) fills roofline.traffic
+PROFILE = {"c3": os.path.join(ROOT, "profiles", "LATEST"), "c5": os.path.join(ROOT, "profiles", "LATEST_C5")}
 
 
-def measured_traffic(kernel_prefix, frames, avg_ms=None):
+def _profile_rows(workload, kernel_prefix, key):
+    try:
+        tag = open(PROFILE[workload]).read().strip()
+        summ = json.load(open(os.path.join(ROOT, "profiles", tag, "summary.json")))
+    except (OSError, ValueError):
+        return None, []
+    return tag, [(n, r) for n, r in summ.items() if kernel_prefix in n and r.get(key) and r.get("isolated_dispatches")]
+
+
+def measured_traffic(workload, kernel_prefix, frames, avg_ms=None):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary, or None
     when no summary exists for this batch size (PMC counters cannot be read inside the run)."""
+    tag, rows = _profile_rows(workload, kernel_prefix, "traffic_gb")
+    if tag is None:
+        return None, None
     try:
-        tag = open(PROFILE).read().strip()
-        summ = json.load(open(os.path.join(ROOT, "profiles", tag, "summary.json")))
         lines = open(os.path.join(ROOT, "profiles", tag, "bench.json")).read().splitlines()
         meta = json.loads([ln for ln in lines if ln.startswith("{")][-1])
     except (OSError, ValueError, IndexError):
-        return None, None
+        return None, tag
     if int(meta.get("config", {}).get("pictures_per_gpu", -1)) != frames:
+        return None, tag
+    if not rows:
         return None, tag
     # the row kernel comes in several builds (alone / overlapped runs): take the profiled one
     # whose isolated duration is closest to this run's launches
-    rows = [(name, row) for name, row in summ.items()
-            if kernel_prefix in name and row.get("traffic_gb") and row.get("isolated_dispatches")]
-    if not rows:
-        return None, tag
     name, row = min(rows, key=lambda nr: abs(nr[1]["avg_ms"] - (avg_ms or 0)))
-    # only valid for the kernel build that was profiled: its duration must agree
     if avg_ms and abs(row["avg_ms"] - avg_ms) > 0.1 * avg_ms:
         return None, tag + " (stale: profiled %.2f ms/launch)" % row["avg_ms"]
     return int(row["traffic_gb"] * 1e9), "%s, %s" % (tag, name.replace("void ", ""))
@@ -59,16 +78,11 @@ VALU_PEAK = 1024 * 2.4e9 / 2.0      # wave-instructions / s
 SALU_PEAK = 256 * 2.4e9             # instructions / s
 
 
-def issue_rates(kernel_prefix, avg_ms):
+def issue_rates(workload, kernel_prefix, avg_ms):
     """Instruction-issue view of the dominant kernel (it is issue-bound): VALU and
     SALU instructions per launch from the committed PMC summary (SQ_INSTS_VALU / SQ_INSTS_SALU of
     the profiled build whose duration matches), divided by this run's launch time and the peaks."""
-    try:
-        tag = open(PROFILE).read().strip()
-        summ = json.load(open(os.path.join(ROOT, "profiles", tag, "summary.json")))
-    except (OSError, ValueError):
-        return None
-    rows = [(n, r) for n, r in summ.items() if kernel_prefix in n and r.get("SQ_INSTS_VALU") and r.get("isolated_dispatches")]
+    tag, rows = _profile_rows(workload, kernel_prefix, "SQ_INSTS_VALU")
     if not rows:
         return None
     name, row = min(rows, key=lambda nr: abs(nr[1]["avg_ms"] - avg_ms))
@@ -87,8 +101,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--frames", type=int, default=512, help="1080p pictures per GPU per step")
-    ap.add_argument("--unique", type=int, default=4, help="distinct synthetic pictures per rank (replicated)")
+    ap.add_argument("--workload", choices=("c3", "c5"), default="c3")
+    ap.add_argument("--frames", type=int, default=512, help="c3: 1080p pictures per GPU per step")
+    ap.add_argument("--unique", type=int, default=4, help="c3: distinct synthetic pictures per rank (replicated)")
+    ap.add_argument("--c5-frames", type=int, default=2, help="c5: 4K frames per step (x4 tile units, all ranks)")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="resident batches run round-robin on this many HIP streams (p265r_set_pipeline): one "
                          "batch's residual / loop-filter phases overlap another's intra phase")
@@ -97,7 +113,40 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the bitstream -> planes end-to-end leg")
     ap.add_argument("--deblocking", action="store_true",
                     help="deblocking on in every slice (real-stream config; SURVEY §8(d) defines the bench without it)")
+    ap.add_argument("--experiment", action="store_true",
+                    help="allow P265R_* library knobs in the environment (recorded in the line; not a headline run)")
     return ap.parse_args()
+
+
+def experiment_env():
+    return {k: v for k, v in os.environ.items() if k.startswith("P265R_")}
+
+
+def host_info():
+    """CPU model, the machine's logical CPUs and this job's CPU share (cgroup quota / affinity)."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    total = os.cpu_count() or 1
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            share = min(share, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    # the GPU pool grants a fixed CPU share per GPU and announces it in OMP_NUM_THREADS (16);
+    # os.cpu_count() there is the whole machine's
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        share = min(share, int(omp))
+    return {"cpu_model": model, "host_cores_total": total, "cpu_share": share}
 
 
 def algorithmic_bytes(pics):
@@ -120,10 +169,9 @@ def algorithmic_bytes(pics):
     return tot, intra, resid, sao
 
 
-def cpu_baseline_python(procs, timeout_s=600):
+def cpu_baseline_python(procs, timeout_s=900):
     """The pure-Python restatement (oracle/py_baseline.py) in a child process that never
     touches the GPU: one 1080p picture per worker, ``procs`` workers."""
-    import subprocess
     r = subprocess.run([sys.executable, "-m", "oracle.py_baseline", "--procs", str(procs)], cwd=ROOT,
                        capture_output=True, text=True, timeout=timeout_s)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -132,31 +180,11 @@ def cpu_baseline_python(procs, timeout_s=600):
     return json.loads(lines[-1])
 
 
-def hbm_copy_gbs(device, nbytes=4 << 30, reps=10):
-    """Achievable HBM bandwidth on this box: a device-to-device copy (read + write bytes / time)."""
-    import torch
-    x = torch.empty(nbytes, dtype=torch.uint8, device=device)
-    y = torch.empty_like(x)
-    y.copy_(x)
-    torch.cuda.synchronize(device)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        y.copy_(x)
-    e1.record()
-    torch.cuda.synchronize(device)
-    ms = e0.elapsed_time(e1) / reps
-    del x, y
-    torch.cuda.empty_cache()
-    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
-
-
-def cpu_baseline(params, uniq, budget_s):
+def cpu_baseline(params, uniq, budget_s, threads, what):
     """CPU oracle (oracle/recon_oracle.c, test infrastructure used here only as the reported
-    baseline) on a bounded sample of the same workload: whole synthetic 1080p pictures,
-    repeated until ~budget_s of wall time, OpenMP over pictures on the host cores."""
+    baseline) on a bounded sample of the same workload: whole pictures (or tile units),
+    repeated until ~budget_s of wall time, OpenMP over pictures on ``threads`` host cores."""
     from oracle import c_oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
     c_oracle.decode(params, uniq[:1], threads=1, with_recon=False)           # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
@@ -166,8 +194,8 @@ def cpu_baseline(params, uniq, budget_s):
     dt = time.perf_counter() - t0
     ctus = n * len(uniq[0].ctus)
     return {"value": round(ctus / dt, 1), "unit": "CTU/s", "cores": threads, "kind": "port",
-            "sample": "oracle/recon_oracle.c (scalar C restatement, OpenMP over pictures): %d synthetic 1080p "
-                      "pictures = %d CTUs in %.1f s" % (n, ctus, dt)}
+            "sample": "oracle/recon_oracle.c (scalar C restatement, OpenMP over pictures): %d synthetic %s "
+                      "= %d CTUs in %.1f s" % (n, what, ctus, dt)}
 
 
 def end_to_end(device, reps=16, threads=16):
@@ -201,26 +229,71 @@ def end_to_end(device, reps=16, threads=16):
             "note": "native front-end (libp265fe.so) on host threads + PCIe-inclusive GPU decode; not `value`"}
 
 
+def build_workload(a, rank, world):
+    """-> (params of the batch pictures, [pictures of this rank], cpu-baseline sample, config dict)."""
+    from p265_amd import dist, synth, tiles
+    from p265_amd import records as R
+    if a.workload == "c3":
+        params = R.make_params(pic_width=1920, pic_height=1080)
+        params = dist.broadcast_params(params)                  # RCCL broadcast of the SPS/PPS POD
+        uniq = [synth.make_picture(params, 268 + 1000 * rank + i, perf=True, deblocking=a.deblocking)
+                for i in range(a.unique)]
+        for p in uniq:
+            p.meta["samples"] = 1920 * 1080 * 3 // 2
+        pics = [uniq[i % a.unique] for i in range(a.frames)]
+        cfg = {"workload": "C3/C4: 1080p all-intra + %sSAO, %d pictures per GPU per step (%d distinct)"
+                           % ("deblocking + " if a.deblocking else "", a.frames, a.unique),
+               "pictures_per_gpu": a.frames, "ctus_per_picture": len(pics[0].ctus), "ctb": 64,
+               "parallelism": "picture-sharded x%d (picture f -> rank f mod N)" % world}
+        return params, pics, (uniq, "1080p pictures"), cfg
+    # C5: 4K, uniform 2x2 tiles, loop_filter_across_tiles 0: every (frame, tile) unit is a
+    # 1920x1080 sub-picture of its own (p265_amd/tiles.py); units dealt to ranks
+    p4k = R.make_params(pic_width=3840, pic_height=2160, loop_filter_across_tiles=0)
+    p4k = dist.broadcast_params(p4k)
+    frames = [synth.make_picture(p4k, 4000 + f, perf=True, tiles=(2, 2), deblocking=a.deblocking)
+              for f in range(a.c5_frames)]
+    mine = dist.unit_shard(a.c5_frames, 4, rank, world)
+    parts = {f: tiles.split(p4k, frames[f]) for f in sorted({f for f, _ in mine})}
+    pics = []
+    params = None
+    for f, t in mine:
+        tp, tpic, _ = parts[f][t]
+        if params is None:
+            params = tp
+        elif tp.tobytes() != params.tobytes():
+            raise RuntimeError("c5: tile units of unequal size")
+        tpic.meta["samples"] = int(tp["pic_width"]) * int(tp["pic_height"]) * 3 // 2
+        pics.append(tpic)
+    if not pics:
+        raise RuntimeError("c5: rank %d has no tile unit (more ranks than units)" % rank)
+    cfg = {"workload": "C5: 4K all-intra + %sSAO (CTU-row SAO kernel), 2x2 uniform tiles x %d frames = %d tile units "
+                       "per step over all ranks, %d on this rank" % ("deblocking + " if a.deblocking else "", a.c5_frames,
+                                                                     4 * a.c5_frames, len(pics)),
+           "pictures_per_gpu": len(pics), "units_per_step": 4 * a.c5_frames,
+           "ctus_per_picture": len(pics[0].ctus), "tile": "%dx%d" % (int(params["pic_width"]), int(params["pic_height"])),
+           "ctb": 64, "parallelism": "(frame, tile) units -> ranks x%d (dist.unit_shard)" % world}
+    return params, pics, (pics, "1920x1080 tile units of 4K frames"), cfg
+
+
 def main():
     a = parse()
-    import torch  # noqa: F401  (loads the HIP runtime libp265r.so binds to; see p265_amd/_lib.py)
-    from p265_amd import dist, recon, synth
-    from p265_amd import records as R
+    exp = experiment_env()
+    if exp and not a.experiment:
+        sys.stderr.write("bench.py: refusing to run with library experiment knobs set: %s "
+                         "(unset them, or pass --experiment for a non-headline run)\n" % sorted(exp))
+        sys.exit(2)
+    from p265_amd import dist, hip, recon
 
+    host = host_info()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     # pure-Python CPU baseline first, in a child process, before this process touches the GPU
     py_base = None
-    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not a.no_cpu_baseline:
-        py_base = cpu_baseline_python(max(1, min(16, os.cpu_count() or 1)))
-    rank, world, local = dist.init("nccl")
-    params = R.make_params(pic_width=1920, pic_height=1080)
-    params = dist.broadcast_params(params)                  # RCCL broadcast of the SPS/PPS POD
+    if world_env == 1 and not a.no_cpu_baseline and a.workload == "c3":
+        py_base = cpu_baseline_python(host["cpu_share"])
+    rank, world, local = dist.init(device=int(os.environ.get("LOCAL_RANK", "0")), rccl=world_env > 1)
 
     t0 = time.time()
-    uniq = [synth.make_picture(params, 268 + 1000 * rank + i, perf=True, deblocking=a.deblocking)
-            for i in range(a.unique)]
-    for p in uniq:
-        p.meta["samples"] = 1920 * 1080 * 3 // 2
-    pics = [uniq[i % a.unique] for i in range(a.frames)]
+    params, pics, (cpu_sample, cpu_what), cfg = build_workload(a, rank, world)
     gen_s = time.time() - t0
 
     ctx = recon.ReconContext(params, device=local)
@@ -231,16 +304,16 @@ def main():
     for k in range(a.warmup):
         ctx.run(batches[k % a.pipeline])
     ctx.sync()
+    hip.synchronize()
     dist.barrier()
-    torch.cuda.synchronize()
-    ctx.sync()
     t_start = time.perf_counter()
     for k in range(a.steps):               # queued back to back, batches alternating over the streams
         ctx.run(batches[k % a.pipeline])
     ctx.sync()
-    torch.cuda.synchronize()
+    hip.synchronize()
+    elapsed_local = time.perf_counter() - t_start
     dist.barrier()
-    elapsed = dist.max_over_ranks(time.perf_counter() - t_start)
+    elapsed = dist.max_over_ranks(elapsed_local)
     # phase breakdown + roofline: the same steps on ONE batch (one stream, no overlap), HIP events
     # around each phase, so every kernel's duration is its own
     ctx.set_timing(True)
@@ -250,26 +323,25 @@ def main():
     ctx.set_timing(False)
     acc = ctx.timings_total()
     assert acc["runs"] == a.steps
+    knobs = ctx.describe()
 
-    total_ctus = world * a.frames * n_ctu * a.steps
+    total_ctus = (world * len(pics) if a.workload == "c3" else 4 * a.c5_frames) * n_ctu * a.steps
     value = total_ctus / elapsed
     tot_b, intra_b, res_b, sao_b = algorithmic_bytes(pics)
     launches_per_step = acc["intra_launches"] / a.steps
     avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     bytes_per_launch = intra_b / launches_per_step
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    traffic, prof_tag = measured_traffic("intra_rows_kernel", a.frames, avg_launch_ms)
+    traffic, prof_tag = measured_traffic(a.workload, "intra_rows_kernel", len(pics), avg_launch_ms)
+    cfg.update(batch_pipeline=a.pipeline, library=knobs)
     out = {
         "metric": METRIC,
         "value": round(value, 1), "unit": "CTU/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak" if a.workload == "c3" else "strong",
         "vs_baseline": None, "dtype": "u8 samples / int16 coefficients (integer)",
         "data": "synthetic: seeded all-intra records with sanity.bin statistics (p265_amd/synth.py)",
-        "config": {"workload": "C3/C4: 1080p all-intra + %sSAO, %d pictures per GPU per step (%d distinct)"
-                               % ("deblocking + " if a.deblocking else "", a.frames, a.unique),
-                   "pictures_per_gpu": a.frames, "ctus_per_picture": n_ctu, "ctb": 64,
-                   "batch_pipeline": a.pipeline,
-                   "parallelism": "picture-sharded x%d" % world},
+        "config": cfg,
         "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
@@ -277,28 +349,38 @@ def main():
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
                      "note": "instruction-issue-bound (VALU + the CU's one scalar unit), not HBM-bound: see "
                              "issue_rates and DESIGN.md §4"},
-        "issue_rates": issue_rates("intra_rows_kernel", avg_launch_ms),
+        "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms),
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
         "phase_gbs": {"residual": round(res_b / (acc["residual_ms"] / a.steps * 1e-3) / 1e9, 1),
                       "sao": round(sao_b / (acc["sao_ms"] / a.steps * 1e-3) / 1e9, 1) if acc["sao_ms"] else None,
                       "whole_path_algorithmic": round(tot_b / (elapsed / a.steps) / 1e9, 2)},
         "setup_s": round(gen_s, 1),
     }
+    if a.workload == "c5":
+        out["unit_latency_ms"] = {
+            "one_batch_step": round(acc["total_ms"] / a.steps, 4),
+            "note": "the %d tile units of a rank's step run concurrently (one workgroup per unit in the intra "
+                    "kernel), so a unit's latency is the one-batch step time; pipelined steps overlap" % len(pics)}
+    if exp:
+        out["experiment_env"] = exp
     if rank == 0:
-        out["roofline"]["achievable_copy_gbs"] = hbm_copy_gbs(local)
+        out["roofline"]["achievable_copy_gbs"] = hip.copy_bandwidth_gbs(local)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = py_base
-        out["cpu_baseline_c"] = cpu_baseline(params, uniq, a.cpu_baseline_seconds)
+        if py_base is not None:
+            py_base.update(host_cores_total=host["host_cores_total"], cpu_model=host["cpu_model"])
+            out["cpu_baseline"] = py_base
+        cb = cpu_baseline(params, cpu_sample, a.cpu_baseline_seconds, host["cpu_share"], cpu_what)
+        cb.update(host_cores_total=host["host_cores_total"], cpu_model=host["cpu_model"])
+        out["cpu_baseline_c" if py_base is not None else "cpu_baseline"] = cb
+    out["host"] = host
     for b in batches:
         b.free()
     ctx.close()
-    if rank == 0 and world == 1 and not a.no_e2e:
-        out["end_to_end"] = end_to_end(local)
+    if rank == 0 and world == 1 and not a.no_e2e and a.workload == "c3":
+        out["end_to_end"] = end_to_end(local, threads=min(16, host["cpu_share"]))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as tdist
-        tdist.destroy_process_group()
+    dist.finalize()
 
 
 if __name__ == "__main__":

@@ -181,6 +181,12 @@ int  p265r_set_timing(p265r_ctx* ctx, int enable);
 int  p265r_last_timings(p265r_ctx* ctx, p265r_timings* out);
 int  p265r_timings_total(p265r_ctx* ctx, p265r_timings* out, int* n_runs);
 
+/* Effective configuration of a context as a JSON object (intra schedule, waves per workgroup,
+ * loop-filter kernel choice, pipeline depth, and which P265R_* environment knobs overrode the
+ * defaults): writes at most size-1 bytes + NUL into buf, returns the full length (like snprintf)
+ * or an error code.  Lets a benchmark record what it measured. */
+int  p265r_describe(p265r_ctx* ctx, char* buf, int size);
+
 /* Number of HIP devices visible (>= 0), or an error code. */
 int  p265r_device_count(void);
 const char* p265r_strerror(int code);

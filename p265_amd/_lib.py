@@ -5,9 +5,11 @@ The library is built in-tree (``make`` or ``__graft_entry__.build()``) and loade
 load, every entry point raises ``LibraryNotFound`` -- the product path never silently
 degrades to a CPU implementation.
 
-If PyTorch is importable it is imported first: its wheel bundles its own
-libamdhip64.so.7, and loading ours first would put two HIP runtimes in one process.
-With torch loaded first, the dynamic linker binds libp265r.so to that same runtime.
+The product path does not use PyTorch: libp265r.so binds the system HIP runtime
+(RUNPATH /opt/rocm-7.2.0/lib), the same file p265_amd/hip.py and p265_amd/rccl.py load.
+A host that also uses PyTorch must load torch BEFORE this library (the torch wheel
+bundles its own libamdhip64 under another file name; imported first, the dynamic linker
+binds libp265r.so to that one runtime instead of loading a second).
 """
 import ctypes
 import os
@@ -80,6 +82,7 @@ SIGNATURES = {
     "p265r_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "p265r_last_hip_error": (ctypes.c_char_p, []),
     "p265r_abi_version": (ctypes.c_uint32, []),
+    "p265r_describe": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
 }
 
 _lib = None
@@ -94,10 +97,6 @@ def load():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise LibraryNotFound("%s not built: run `make` or __graft_entry__.build()" % LIB_PATH)
-        try:
-            import torch  # noqa: F401  (bind to the HIP runtime torch already ships, see module doc)
-        except Exception:
-            pass
         try:
             lib = ctypes.CDLL(LIB_PATH)
         except OSError as e:

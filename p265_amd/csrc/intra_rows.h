@@ -147,7 +147,7 @@ struct RowCtrl {                 // 256 B at the start of dynamic LDS
 // half empty for the younger one's tail.  Each workgroup takes a rank in its CU's slot (one
 // atomic add at start; slot = XCC id x 128 + CU / SH / SE id), publishes the rows it has
 // dequeued, and at every row start runs at priority 1 while it is behind its partner.
-constexpr int kRowCuSlots = 1024;
+constexpr int kRowCuSlots = 2048;
 struct RowCuSlot { int count; int prog[3]; };
 // Dynamic LDS layout: [RowCtrl 256 B][prog: fs x hc ints][W x WaveLds][fs x 2 line buffers]
 // prog[slot][cy] = (local picture index & 0xffff) << 16 | CTUs done.
@@ -786,11 +786,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            Geo g, int n_pics, int fs_count, int lead,
                                                            int* __restrict__ err_flag,
                                                            int* __restrict__ dbg) {
-    // debug trace (P265R_DEBUG_SYNC=1): host-mapped words, one per wave
-#if defined(P265R_DBG_NOTRACE)
-#define P265R_TRACE(code) do { } while (0)
-#else
+    // debug trace (P265R_DEBUG_DIAG builds, P265R_DEBUG_SYNC=1): host-mapped words, one per wave
+#if defined(P265R_DEBUG_DIAG) && !defined(P265R_DBG_NOTRACE)
 #define P265R_TRACE(code) do { if (dbg && lane == 0) __hip_atomic_store(dbg + blockIdx.x * W + wave, (code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#else
+#define P265R_TRACE(code) do { } while (0)
 #endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     RowCtrl& ctl = *reinterpret_cast<RowCtrl*>(smem);
@@ -812,7 +812,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             uint32_t xcc, hwid;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-            const int key = (int)((xcc & 7u) * 128u + ((hwid >> 8) & 127u));      // CU_ID, SH_ID, SE_ID
+            const int key = (int)((xcc & 7u) * 256u + ((hwid >> 8) & 255u));      // CU_ID, SH_ID, SE_ID (3 bits)
             RowCuSlot* cs = reinterpret_cast<RowCuSlot*>(err_flag + 64) + key;
             ctl.cu_slot = key;
             ctl.cu_rank = __hip_atomic_fetch_add(&cs->count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1;
@@ -832,13 +832,20 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     const int ctb = 1 << g.ctb_log2;
     // bounded spin-wait on an LDS word; false = gave up (error published, caller bails out).
     // Every condition is made wave-uniform (readfirstlane) so the loops are scalar loops.
+#ifdef P265R_DEBUG_DIAG
     long long t_wait = 0;
     const long long t_begin = __builtin_amdgcn_s_memtime();
+#define P265R_WAIT_T0 const long long t0 = __builtin_amdgcn_s_memtime()
+#define P265R_WAIT_ADD t_wait += __builtin_amdgcn_s_memtime() - t0
+#else
+#define P265R_WAIT_T0 do { } while (0)
+#define P265R_WAIT_ADD do { } while (0)
+#endif
     auto wait_until = [&](auto ready) -> bool {
-        const long long t0 = __builtin_amdgcn_s_memtime();
+        P265R_WAIT_T0;
         for (int spins = 0; spins < (1 << 24); ++spins) {
             if (spins == 0 && __builtin_amdgcn_readfirstlane((int)ready())) return true;
-            if (__builtin_amdgcn_readfirstlane((int)ready())) { t_wait += __builtin_amdgcn_s_memtime() - t0; return true; }
+            if (__builtin_amdgcn_readfirstlane((int)ready())) { P265R_WAIT_ADD; return true; }
             if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 return false;
             __builtin_amdgcn_s_sleep(P265R_SPIN_SLEEP);   // 64 cycles per unit; each poll costs issue slots
@@ -1113,6 +1120,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     if (dbg && threadIdx.x < 28)
         atomicAdd(dbg + 3 * gridDim.x * W + 2 * gridDim.x + threadIdx.x, ctl.pad[threadIdx.x]);
 #endif
+#ifdef P265R_DEBUG_DIAG
     if (dbg) {   // debug statistics: [total cycles, cycles in dependency waits] per wave
         const long long t_all = __builtin_amdgcn_s_memtime() - t_begin;
         const int slotw = gridDim.x * W + 2 * (blockIdx.x * W + wave);
@@ -1127,6 +1135,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             __hip_atomic_store(dbg + slotp + 1, (int)hwid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+#endif
+    (void)dbg;
     // all stores of this wave are issued before it ends (compiler barrier)
     asm volatile("" ::: "memory");
 }

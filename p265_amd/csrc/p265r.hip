@@ -97,7 +97,8 @@ struct p265r_ctx {
     int luma_lead = 5;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
                                // measured, 1080p W=8: lead 0/1/2/3/5/8/17 -> 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
     int num_cus = 256;
-    bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every launch
+    bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every phase (P265R_DEBUG_DIAG
+                               // builds also trace the row kernel's waves and print placement statistics)
     // reused across batches: pinned host staging (grow-only) and one freed device allocation
     unsigned char* stage = nullptr;
     size_t stage_bytes = 0;
@@ -110,18 +111,7 @@ struct p265r_ctx {
     int pipeline = 1;
     int next_lane = 0;
     std::vector<hipStream_t> lanes;   // lanes[0] == stream
-    // with P265R_PRIO=1 each lane's intra kernel runs on a high-priority twin stream
-    // (ordered against the lane by events), so freed CU slots go to the long intra kernels first
-    // (measured, 512 x 1080p: 3 lanes 12.10-12.15 -> 12.42-12.51 ms/step, 2 lanes 12.30 -> 12.01;
-    // off by default)
-    // P265R_PRIO=2: one shared intra stream instead (normal priority): the intra kernels of
-    // all lanes run one after another while residual / loop-filter phases run beside them
-    // P265R_PRIO=3: per lane a normal-priority twin runs intra + in-loop filters, so the lane
-    // starts the next batch's residual / prep phases while this batch's filters still run (the
-    // lane waits only for the previous run's intra kernel, which reads the residuals)
-    int prio = 0;
-    std::vector<hipStream_t> lanes_hi;
-    std::vector<hipEvent_t> lane_ev;  // 2 per lane: residual phase done, intra phase done
+    std::string describe;             // p265r_describe text
 };
 
 struct p265r_batch {
@@ -136,15 +126,11 @@ struct p265r_batch {
     int n_jobs[RC_NUM] = {};
     std::vector<DevPic> h_pics;
     hipStream_t stream = nullptr;  // the context lane this batch runs on
-    hipStream_t stream_hi = nullptr;  // its high-priority twin (intra phase), or null
     int lane = 0;
-    hipStream_t intra_stream = nullptr;  // where launch_rows enqueues (set by batch_run)
     bool sao = false;
     bool dbk = false;          // some CTU of the batch has deblocking on
     bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
     int runs = 0;              // p265r_batch_run calls so far
-    hipEvent_t intra_done = nullptr;  // P265R_PRIO=3: its last intra phase (on the twin stream)
-    bool intra_pending = false;
 };
 
 namespace {
@@ -212,10 +198,59 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     return P265R_OK;
 }
 
+#ifdef P265R_DEBUG_DIAG
+// Row-kernel diagnostics (P265R_DEBUG_DIAG builds with P265R_DEBUG_SYNC=1): wave trace of a hung
+// launch, dependency-wait share, workgroup lifetimes and placement, per-job-class cycles
+// (P265R_JOB_STATS builds).  Not compiled into the product library.
+void rows_diag(hipStream_t st, const int* dbg, int grid, int W) {
+    for (int it = 0; it < 100; ++it) {
+        if (hipStreamQuery(st) == hipSuccess) break;
+        struct timespec ts{0, 100000000};
+        nanosleep(&ts, nullptr);
+        if (it == 99) {
+            fprintf(stderr, "[p265r] rows kernel still running after 10 s; wave trace:\n");
+            for (int i = 0; i < grid * W && i < 64; ++i) fprintf(stderr, "  wg %d wave %d: code %d (0x%x)\n", i / W, i % W, dbg[i] & 0xff, dbg[i]);
+            fflush(stderr);
+            std::abort();
+        }
+    }
+    double tot = 0, wt = 0;
+    for (int i = 0; i < grid * W; ++i) { tot += dbg[grid * W + 2 * i]; wt += dbg[grid * W + 2 * i + 1]; }
+    fprintf(stderr, "[p265r] rows kernel: %.1f%% of wave time in dependency waits (%d waves)\n", 100.0 * wt / (tot > 0 ? tot : 1), grid * W);
+    std::vector<int> life(grid, 0);          // workgroup lifetimes (longest wave, 256-cycle units)
+    for (int i = 0; i < grid * W; ++i) life[i / W] = std::max(life[i / W], dbg[grid * W + 2 * i]);
+    double sx[16] = {}; int nx[16] = {};
+    for (int i = 0; i < grid; ++i) { const int x = dbg[3 * grid * W + 2 * i] & 15; sx[x] += life[i]; ++nx[x]; }
+    fprintf(stderr, "[p265r] mean workgroup lifetime per XCC (Mcycles):");
+    for (int x = 0; x < 16; ++x) if (nx[x]) fprintf(stderr, " x%d:%.2f(%d)", x, sx[x] / nx[x] * 256e-6, nx[x]);
+    fprintf(stderr, "\n");
+    std::vector<std::pair<int, int>> byhw;
+    for (int i = 0; i < grid; ++i) byhw.push_back({dbg[3 * grid * W + 2 * i] * 256 + ((dbg[3 * grid * W + 2 * i + 1] >> 8) & 255), life[i]});
+    std::sort(byhw.begin(), byhw.end());
+    int same = 0; double dsum = 0;
+    for (size_t i = 1; i < byhw.size(); ++i)
+        if (byhw[i].first == byhw[i - 1].first) { ++same; dsum += std::abs(byhw[i].second - byhw[i - 1].second); }
+    fprintf(stderr, "[p265r] workgroups sharing a CU: %d pairs, mean lifetime difference %.2f Mcycles\n", same, same ? dsum / same * 256e-6 : 0.0);
+    static const char* names[14] = {"luma quad", "chroma quad", "fast Y4", "fast Y8", "fast Y16", "fast C4 pair",
+                                    "fast C8 pair", "gen Y4", "gen Y8", "gen Y16", "gen Y32", "gen C4", "gen C8", "gen C16"};
+    const int* js = dbg + 3 * grid * W + 2 * grid;
+    double jt = 0;
+    for (int k = 0; k < 14; ++k) jt += 16.0 * (unsigned)js[2 * k];
+    for (int k = 0; k < 14; ++k)
+        if (js[2 * k + 1])
+            fprintf(stderr, "[p265r] jobs %-13s %9d  %7.0f cycles/job  %5.1f %%\n", names[k], js[2 * k + 1],
+                    16.0 * (unsigned)js[2 * k] / js[2 * k + 1], 100.0 * 16.0 * (unsigned)js[2 * k] / (jt > 0 ? jt : 1));
+    std::sort(life.begin(), life.end());
+    if (grid > 0)
+        fprintf(stderr, "[p265r] rows kernel workgroup lifetime (Mcycles): min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+                life[0] * 256e-6, life[grid / 10] * 256e-6, life[grid / 2] * 256e-6, life[grid * 9 / 10] * 256e-6,
+                life[grid - 1] * 256e-6);
+}
+#endif
+
 template <int W, int WPE>
-int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, bool alone) {
+int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     Geo g = ctx->geo;
-    g.fair = g.fair && alone;
     // picture slots: the W rows in flight are consecutive in the queue, so they span at
     // most ceil(W / hc) + 1 pictures; a slot is reused only after its previous picture is
     // complete (the kernel waits for that, so fewer slots would still be correct)
@@ -241,84 +276,44 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, bool alone) {
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds));
     if (per_cu < 1) return P265R_EUNSUPPORTED;
     const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
+    // fair CU sharing pairs the two workgroups of a CU (rank = arrival order & 1): only valid
+    // when exactly two fit per CU and all of them are resident for the whole launch (grid <= 2
+    // per CU, no workgroup starts after another ends) -- and only worth it for a batch alone
+    g.fair = g.fair && alone && per_cu == 2;
     int* dbg = nullptr;
+#ifdef P265R_DEBUG_DIAG
     if (ctx->debug_sync) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&dbg), sizeof(int) * (grid * W * 3 + grid * 2 + 32), hipHostMallocMapped | hipHostMallocCoherent));
         std::memset(dbg, 0, sizeof(int) * (grid * W * 3 + grid * 2 + 32));
         fprintf(stderr, "[p265r] rows kernel W=%d WPE=%d fair=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, WPE, g.fair, grid, lds, fs, per_cu);
     }
-    fn<<<grid, 64 * W, lds, b->intra_stream>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
+#endif
+    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
     HIP_TRY(hipGetLastError());
+#ifdef P265R_DEBUG_DIAG
     if (dbg) {
-        for (int it = 0; it < 100; ++it) {
-            if (hipStreamQuery(b->intra_stream) == hipSuccess) break;
-            struct timespec ts{0, 100000000};
-            nanosleep(&ts, nullptr);
-            if (it == 99) {
-                fprintf(stderr, "[p265r] rows kernel still running after 10 s; wave trace:\n");
-                for (int i = 0; i < grid * W && i < 64; ++i) fprintf(stderr, "  wg %d wave %d: code %d (0x%x)\n", i / W, i % W, dbg[i] & 0xff, dbg[i]);
-                fflush(stderr);
-                std::abort();
-            }
-        }
-        double tot = 0, wt = 0;
-        for (int i = 0; i < grid * W; ++i) { tot += dbg[grid * W + 2 * i]; wt += dbg[grid * W + 2 * i + 1]; }
-        fprintf(stderr, "[p265r] rows kernel: %.1f%% of wave time in dependency waits (%d waves)\n", 100.0 * wt / (tot > 0 ? tot : 1), grid * W);
-        // workgroup lifetimes (longest wave of each, 256-cycle units): the kernel ends with the slowest
-        std::vector<int> life(grid, 0);
-        for (int i = 0; i < grid * W; ++i) life[i / W] = std::max(life[i / W], dbg[grid * W + 2 * i]);
-        {   // by XCC and by CU slot: where do the slow workgroups run?
-            double sx[16] = {}; int nx[16] = {};
-            for (int i = 0; i < grid; ++i) { const int x = dbg[3 * grid * W + 2 * i] & 15; sx[x] += life[i]; ++nx[x]; }
-            fprintf(stderr, "[p265r] mean workgroup lifetime per XCC (Mcycles):");
-            for (int x = 0; x < 16; ++x) if (nx[x]) fprintf(stderr, " x%d:%.2f(%d)", x, sx[x] / nx[x] * 256e-6, nx[x]);
-            fprintf(stderr, "\n");
-            std::vector<std::pair<int, int>> byhw;
-            for (int i = 0; i < grid; ++i) byhw.push_back({dbg[3 * grid * W + 2 * i] * 128 + ((dbg[3 * grid * W + 2 * i + 1] >> 8) & 127), life[i]});
-            std::sort(byhw.begin(), byhw.end());
-            int same = 0; double dsum = 0;
-            for (size_t i = 1; i < byhw.size(); ++i)
-                if (byhw[i].first == byhw[i - 1].first) { ++same; dsum += std::abs(byhw[i].second - byhw[i - 1].second); }
-            fprintf(stderr, "[p265r] workgroups sharing a CU: %d pairs, mean lifetime difference %.2f Mcycles\n", same, same ? dsum / same * 256e-6 : 0.0);
-            for (int i = 0; i < 24 && i < grid; ++i)
-                fprintf(stderr, "  wg %d xcc %d hwid 0x%x life %.2f\n", i, dbg[3 * grid * W + 2 * i], dbg[3 * grid * W + 2 * i + 1], life[i] * 256e-6);
-        }
-        {   // per job class (P265R_JOB_STATS builds): jobs, cycles per job
-            static const char* names[14] = {"luma quad", "chroma quad", "fast Y4", "fast Y8", "fast Y16", "fast C4 pair",
-                                            "fast C8 pair", "gen Y4", "gen Y8", "gen Y16", "gen Y32", "gen C4", "gen C8", "gen C16"};
-            const int* js = dbg + 3 * grid * W + 2 * grid;
-            double tot = 0;
-            for (int k = 0; k < 14; ++k) tot += 16.0 * (unsigned)js[2 * k];
-            for (int k = 0; k < 14; ++k)
-                if (js[2 * k + 1])
-                    fprintf(stderr, "[p265r] jobs %-13s %9d  %7.0f cycles/job  %5.1f %%\n", names[k], js[2 * k + 1],
-                            16.0 * (unsigned)js[2 * k] / js[2 * k + 1], 100.0 * 16.0 * (unsigned)js[2 * k] / (tot > 0 ? tot : 1));
-        }
-        std::sort(life.begin(), life.end());
-        if (grid > 0)
-            fprintf(stderr, "[p265r] rows kernel workgroup lifetime (Mcycles): min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
-                    life[0] * 256e-6, life[grid / 10] * 256e-6, life[grid / 2] * 256e-6, life[grid * 9 / 10] * 256e-6,
-                    life[grid - 1] * 256e-6);
+        rows_diag(st, dbg, grid, W);
         (void)hipHostFree(dbg);
     }
+#endif
     return P265R_OK;
 }
 
 // alone: no other lane of the context has work queued, so this batch's kernels have the GPU to
 // themselves (fair CU sharing, the unconstrained W = 8 build); otherwise the register-lean build
-int launch_rows(p265r_ctx* ctx, p265r_batch* b, bool alone) {
+int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     switch (ctx->row_waves) {
         case 0:
-            if (alone) return launch_rows_w<12, 6>(ctx, b, alone);
-            return launch_rows_w<8, 6>(ctx, b, alone);
-        case 4: return launch_rows_w<4, 1>(ctx, b, alone);
-        case 6: return launch_rows_w<6, 1>(ctx, b, alone);
-        case 10: return launch_rows_w<10, 5>(ctx, b, alone);
-        case 12: return launch_rows_w<12, 6>(ctx, b, alone);
-        case 16: return launch_rows_w<16, 1>(ctx, b, alone);
+            if (alone) return launch_rows_w<12, 6>(ctx, b, st, alone);
+            return launch_rows_w<8, 6>(ctx, b, st, alone);
+        case 4: return launch_rows_w<4, 1>(ctx, b, st, alone);
+        case 6: return launch_rows_w<6, 1>(ctx, b, st, alone);
+        case 10: return launch_rows_w<10, 5>(ctx, b, st, alone);
+        case 12: return launch_rows_w<12, 6>(ctx, b, st, alone);
+        case 16: return launch_rows_w<16, 1>(ctx, b, st, alone);
         default:
-            if (ctx->lean == 1 || (ctx->lean < 0 && !alone)) return launch_rows_w<8, 6>(ctx, b, alone);
-            return launch_rows_w<8, 1>(ctx, b, alone);
+            if (ctx->lean == 1 || (ctx->lean < 0 && !alone)) return launch_rows_w<8, 6>(ctx, b, st, alone);
+            return launch_rows_w<8, 1>(ctx, b, st, alone);
     }
 }
 
@@ -384,9 +379,12 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.quad = 3;
     if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 7;
     ctx->n_ctus = g.wc * g.hc;
+    // experiment / test knobs read from the environment (bench.py refuses to run with any set)
+    for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_DEBUG_SYNC", "P265R_SAO_ROWS", "P265R_SKIP",
+                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES"})
+        if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
-    if (const char* v = std::getenv("P265R_PRIO")) { const int pv = std::atoi(v); ctx->prio = pv >= 1 && pv <= 3 ? pv : 0; }
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = v[0] != '0';
     if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
@@ -419,14 +417,10 @@ void p265r_destroy(p265r_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     for (hipStream_t st : ctx->lanes) (void)hipStreamSynchronize(st);
-    for (hipStream_t st : ctx->lanes_hi) (void)hipStreamSynchronize(st);
     if (ctx->pending) p265r_batch_free(ctx, ctx->pending);
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
     for (auto& e : ctx->spare) (void)hipEventDestroy(e);
     for (size_t i = 1; i < ctx->lanes.size(); ++i) (void)hipStreamDestroy(ctx->lanes[i]);
-    for (size_t i = 0; i < ctx->lanes_hi.size(); ++i)                 // (P265R_PRIO=2: one stream, listed per lane)
-        if (i == 0 || ctx->lanes_hi[i] != ctx->lanes_hi[0]) (void)hipStreamDestroy(ctx->lanes_hi[i]);
-    for (hipEvent_t ev : ctx->lane_ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
     if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
@@ -557,7 +551,6 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     if (ctx->pipeline > 1) {
         b->lane = ctx->next_lane++ % ctx->pipeline;
         b->stream = ctx->lanes[b->lane];
-        if (ctx->prio) b->stream_hi = ctx->lanes_hi[b->lane];
     }
     b->sao = sao;
     b->dbk = dbk;
@@ -685,8 +678,6 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     hipStream_t s = b->stream;
     const Geo& g = ctx->geo;
     p265r_timings tm{};
-    const bool twin_lf = b->stream_hi && ctx->prio == 3;   // filters stay on the twin (P265R_PRIO=3)
-    if (twin_lf && b->intra_pending) HIP_TRY(hipStreamWaitEvent(s, b->intra_done, 0));   // residuals free
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (ctx->timing) {
         for (auto& e : ev) {
@@ -742,23 +733,19 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] residual phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] residual phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[1], s));
     // ---- intra wavefront ---------------------------------------------------------------
-    const hipStream_t s_lane = s;
-    if (b->stream_hi) {                          // intra phase on the lane's high-priority twin
-        HIP_TRY(hipEventRecord(ctx->lane_ev[2 * b->lane], s_lane));
-        HIP_TRY(hipStreamWaitEvent(b->stream_hi, ctx->lane_ev[2 * b->lane], 0));
-        s = b->stream_hi;
-    }
-    b->intra_stream = s;
     if (recon && ctx->schedule == 1) {
         HIP_TRY(hipMemsetAsync(b->d_err, 0, 256 + kRowCuSlots * 16, s));
-        // does another lane still have work queued (batches overlapping)?
+        // does another lane still have work queued (batches overlapping)?  hipErrorNotReady is
+        // "busy"; any other error (e.g. a fault in another lane's kernel) is reported, not cleared
         bool alone = true;
-        for (size_t i = 0; i < ctx->lanes.size(); ++i)
-            if ((int)i != b->lane && hipStreamQuery(ctx->lanes[i]) != hipSuccess) alone = false;
-        for (size_t i = 0; i < ctx->lanes_hi.size(); ++i)
-            if (ctx->lanes_hi[i] != s && hipStreamQuery(ctx->lanes_hi[i]) != hipSuccess) alone = false;
-        (void)hipGetLastError();                    // hipStreamQuery's hipErrorNotReady is not an error
-        int rc = launch_rows(ctx, b, alone);
+        for (size_t i = 0; i < ctx->lanes.size(); ++i) {
+            if ((int)i == b->lane) continue;
+            const hipError_t q = hipStreamQuery(ctx->lanes[i]);
+            if (q == hipErrorNotReady) alone = false;
+            else if (q != hipSuccess) return hip_fail(q, "hipStreamQuery");
+        }
+        (void)hipGetLastError();                    // drop the sticky hipErrorNotReady of the queries
+        int rc = launch_rows(ctx, b, s, alone);
         if (rc) return rc;
         ++tm.intra_launches;
     }
@@ -775,15 +762,6 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     HIP_TRY(hipGetLastError());
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
-    if (twin_lf) {                               // filters follow on the twin; mark the residuals free
-        if (!b->intra_done) HIP_TRY(hipEventCreateWithFlags(&b->intra_done, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(b->intra_done, s));
-        b->intra_pending = true;
-    } else if (s != s_lane) {                    // back to the lane: loop filters after the intra phase
-        HIP_TRY(hipEventRecord(ctx->lane_ev[2 * b->lane + 1], s));
-        HIP_TRY(hipStreamWaitEvent(s_lane, ctx->lane_ev[2 * b->lane + 1], 0));
-        s = s_lane;
-    }
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
     if (b->sao && !b->dbk && ctx->sao_rows && !(skip & 4)) {
         // SAO only: the streaming SAO kernel (sao_rows.h), one wave per (picture, component, CTB
@@ -836,7 +814,6 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
                                          hipMemcpyDeviceToHost, b->stream));
         }
     HIP_TRY(hipStreamSynchronize(b->stream));
-    if (b->stream_hi) HIP_TRY(hipStreamSynchronize(b->stream_hi));
     int err = 0;
     HIP_TRY(hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
@@ -852,8 +829,6 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->pending == b) ctx->pending = nullptr;
     hipError_t e = hipSuccess;
     if (b->stream && b->stream != ctx->stream) e = hipStreamSynchronize(b->stream);   // its lane may still run it
-    if (b->stream_hi && e == hipSuccess) e = hipStreamSynchronize(b->stream_hi);
-    if (b->intra_done) (void)hipEventDestroy(b->intra_done);
     if (b->mem) {
         // keep the larger of (cache, this allocation) for the next upload; callers free a batch
         // only once its work is complete (download/sync), and reuse is ordered on ctx->stream
@@ -897,7 +872,6 @@ int p265r_sync(p265r_ctx* ctx) {
     if (!ctx) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     for (hipStream_t st : ctx->lanes) HIP_TRY(hipStreamSynchronize(st));
-    for (hipStream_t st : ctx->lanes_hi) HIP_TRY(hipStreamSynchronize(st));
     return P265R_OK;
 }
 
@@ -909,24 +883,36 @@ int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
         HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         ctx->lanes.push_back(st);
     }
-    if (ctx->prio) {
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        while ((int)ctx->lanes_hi.size() < depth) {
-            hipStream_t st = nullptr;
-            if (ctx->prio == 2 && !ctx->lanes_hi.empty()) st = ctx->lanes_hi[0];
-            else HIP_TRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, ctx->prio == 1 ? greatest : least));
-            ctx->lanes_hi.push_back(st);
-            for (int k = 0; k < 2; ++k) {
-                hipEvent_t ev = nullptr;
-                HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-                ctx->lane_ev.push_back(ev);
-            }
-        }
-    }
     ctx->pipeline = depth;
     ctx->next_lane = 0;
     return P265R_OK;
+}
+
+int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
+    if (!ctx || size < 0 || (size > 0 && !buf)) return P265R_EINVAL;
+    const Geo& g = ctx->geo;
+    char tmp[768];
+    const int n = snprintf(tmp, sizeof(tmp),
+        "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
+        "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
+        "\"pipeline\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
+        ctx->schedule ? "rows" : "steps", ctx->row_waves,
+        ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, W=8 register-lean while other lanes have work",
+        ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows ? 1 : 0, ctx->skip, ctx->debug_sync ? 1 : 0,
+        ctx->pipeline, ctx->num_cus,
+#ifdef P265R_DEBUG_DIAG
+        1,
+#else
+        0,
+#endif
+        ctx->describe.c_str());
+    if (n < 0) return P265R_EINVAL;
+    if (size > 0) {
+        const int k = std::min(n, size - 1);
+        std::memcpy(buf, tmp, (size_t)k);
+        buf[k] = 0;
+    }
+    return n;
 }
 
 int p265r_set_timing(p265r_ctx* ctx, int enable) {

@@ -19,8 +19,8 @@ a picture with ``recon_input`` (P265R_PIC_RECON_INPUT: the library skips residua
 intra and runs deblocking + SAO), and keeps the tile's part of the output.
 
 The exchange is a real point-to-point step: ``exchange`` sends each neighbour its
-halo with torch.distributed isend/irecv (RCCL over xGMI with the "nccl" backend; gloo on
-the CPU).  Everything here is host-side plumbing; the filtering runs in libp265r.so.
+halo with ncclSend / ncclRecv (RCCL over xGMI, p265_amd/rccl.py; over the socket control
+plane of p265_amd/comm.py in CPU-only runs).  Everything here is host-side plumbing; the filtering runs in libp265r.so.
 """
 import io
 
@@ -242,39 +242,12 @@ def recon_only(params, pic):
 
 
 # ---------------------------------------------------------------------------------------
-# point-to-point exchange (torch.distributed)
+# point-to-point exchange (RCCL send / recv, p265_amd/dist.py)
 # ---------------------------------------------------------------------------------------
 
-def exchange(sends, recvs, device=None):
-    """sends: [(dst_rank, tag, bytes)], recvs: [(src_rank, tag)] -> {tag: bytes}.
-
-    Two rounds of isend/irecv: the payload lengths (int64), then the payloads (uint8),
-    on ``device`` (a CUDA device with the RCCL backend, CPU with gloo).  Tags order the
-    messages between one pair of ranks (posted in sorted tag order on both sides).
-    """
-    import torch
-    import torch.distributed as dist
-    dev = device or torch.device("cpu")
-    sends = sorted(sends, key=lambda s: (s[0], s[1]))
-    recvs = sorted(recvs, key=lambda r: (r[0], r[1]))
-    ops, lens_in = [], []
-    for dst, tag, data in sends:
-        ops.append(dist.P2POp(dist.isend, torch.tensor([len(data)], dtype=torch.int64, device=dev), dst))
-    for src, tag in recvs:
-        t = torch.zeros(1, dtype=torch.int64, device=dev)
-        lens_in.append(t)
-        ops.append(dist.P2POp(dist.irecv, t, src))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-    ops, bufs = [], []
-    for dst, tag, data in sends:
-        ops.append(dist.P2POp(dist.isend, torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev), dst))
-    for (src, tag), n in zip(recvs, lens_in):
-        b = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
-        bufs.append(b)
-        ops.append(dist.P2POp(dist.irecv, b, src))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-    return {tag: b.cpu().numpy().tobytes() for (src, tag), b in zip(recvs, bufs)}
+def exchange(sends, recvs):
+    """sends: [(dst_rank, tag, bytes)], recvs: [(src_rank, tag)] -> {tag: bytes}, over the
+    process group of p265_amd.dist (ncclSend / ncclRecv on the GPU box; the socket control
+    plane on CPU).  Every rank calls it, also with nothing to send."""
+    from . import dist
+    return dist.exchange(sends, recvs)

@@ -159,6 +159,16 @@ class ReconContext:
         d["runs"] = n.value
         return d
 
+    def describe(self):
+        """Effective configuration of this context (p265r_describe) as a dict."""
+        import json
+        buf = ctypes.create_string_buffer(1024)
+        n = _lib.check(self.lib.p265r_describe(self.handle, buf, len(buf)), "p265r_describe")
+        if n >= len(buf):
+            buf = ctypes.create_string_buffer(n + 1)
+            _lib.check(self.lib.p265r_describe(self.handle, buf, len(buf)), "p265r_describe")
+        return json.loads(buf.value.decode())
+
     def last_timings(self):
         t = _lib.Timings()
         _lib.check(self.lib.p265r_last_timings(self.handle, ctypes.byref(t)), "p265r_last_timings")

@@ -1,0 +1,97 @@
+"""Multi-process product path on the GPU box (named to run FIRST in a -m gpu session, so
+the rank processes start before this process has touched the GPU).
+
+* Two rank processes (tests/multirank_worker.py, plain child processes with a stdlib-socket
+  rendezvous) decode through libp265r.so on device 0: the C4 picture shard, the C5 tile-unit
+  shard of tests/golden/synth_4k_tiles.bin and the C5 halo exchange with
+  loop_filter_across_tiles_enabled_flag = 1.  The gathered results must equal the C oracle /
+  the stream's MD5 SEI.
+* A one-rank RCCL communicator (ctypes librccl.so.1, no PyTorch) broadcasts the params POD
+  through a hipMalloc'd buffer.  Multi-rank RCCL needs one device per rank: it runs in
+  bench.py on an 8-GPU node, not here.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import c_oracle
+from p265_amd import bitstream, halo, synth, tiles
+from p265_amd import records as R
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _planes(path):
+    z = np.load(path)
+    return [z["arr_%d" % c] for c in range(3)]
+
+
+def test_two_rank_processes_decode_their_shards(tmp_path):
+    from ranks import free_port
+    port = free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   P265_CTRL_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "multirank_worker.py"),
+                                       str(tmp_path), "--device", "0"], env=env, cwd=ROOT,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(out)
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)[-3000:]
+    res = json.load(open(tmp_path / "result.json"))
+    assert res["world"] == 2 and res["width"] == 320
+    # C4: every picture decoded once, equal to the oracle
+    params = R.make_params(pic_width=320, pic_height=192)
+    ref = c_oracle.decode(params, [synth.make_picture(params, 900 + f) for f in range(6)], with_recon=False)
+    assert sorted(res["c4"]) == [str(f) for f in range(6)]
+    for f in range(6):
+        assert res["c4"][str(f)] == hashlib.sha256(b"".join(ref[f][1][c].tobytes() for c in range(3))).hexdigest()
+    # C5: 8 tile units over the two ranks, stitched pictures reproduce the MD5 SEI
+    pics = bitstream.decode_stream(open(os.path.join(ROOT, "tests", "golden", "synth_4k_tiles.bin"), "rb").read())
+    assert len(res["c5"]) == 8 and sorted(set(res["c5"].values())) == [0, 1]
+    for f, p in enumerate(pics):
+        parts = tiles.split(p.params, p.picture)
+        full = tiles.stitch(p.params, parts, [_planes(tmp_path / ("c5_%d_%d.npz" % (f, t))) for t in range(len(parts))])
+        assert [hashlib.md5(np.ascontiguousarray(full[c]).tobytes()).digest() for c in range(3)] == p.hash
+    # C5 halo exchange: every tile's filtered output equals whole-picture decoding
+    hp = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, loop_filter_across_tiles=1,
+                       pps_cb_qp_offset=2, pps_cr_qp_offset=-1)
+    hpic = synth.make_picture(hp, 77, perf=False, tiles=(2, 2), n_slices=3, lf_across_slices=None,
+                              deblocking="random", bypass_rate=0.04, pcm_rate=0.02)
+    whole = c_oracle.decode(hp, [hpic], with_recon=False)[0][1]
+    grid = halo.TileGrid.from_picture(hp, hpic)
+    assert sorted(res["halo"]) == [str(t) for t in range(grid.n_tiles)]
+    for t in range(grid.n_tiles):
+        got = _planes(tmp_path / ("halo_%d.npz" % t))
+        x0, x1, y0, y1 = grid.luma_rect(grid.rect(t))
+        for c in range(3):
+            s = 0 if c == 0 else 1
+            np.testing.assert_array_equal(got[c], whole[c][y0 >> s:y1 >> s, x0 >> s:x1 >> s], err_msg="tile %d c%d" % (t, c))
+
+
+def test_rccl_world1_broadcast_of_the_params():
+    from p265_amd import rccl
+    comm = rccl.Rccl(0, 1, 0)
+    try:
+        p = R.make_params(pic_width=1920, pic_height=1080, pps_cb_qp_offset=-3)
+        raw = np.asarray(p, R.PARAMS_DTYPE).tobytes()
+        assert comm.broadcast(raw, root=0) == raw
+        got = comm.exchange({0: b"halo-bytes"}, {0: 10})          # self send / recv in one group
+        assert got == {0: b"halo-bytes"}
+    finally:
+        comm.close()

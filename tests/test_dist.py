@@ -1,9 +1,9 @@
-"""Sharding logic of the multi-GPU path, on CPU: tile sub-pictures (C5) and a
-world_size-2 gloo run of frame sharding (C4) with the params broadcast.  The decode
-inside the ranks uses the C oracle (no GPU here); on the MI355X box bench.py runs the
-same shard plan through libp265r.so with the nccl (RCCL) backend."""
+"""Sharding logic of the multi-GPU path, on CPU: tile sub-pictures (C5), a world_size-2
+run of frame sharding (C4) with the params broadcast over the socket control plane
+(p265_amd/comm.py), and the control-plane collectives with three ranks.  The decode inside
+the ranks uses the C oracle (no GPU here); tests/test_a_multirank.py runs the same shard
+plans through libp265r.so on the GPU box, and bench.py broadcasts the params with RCCL."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -42,12 +42,8 @@ def test_tile_split_refuses_cross_tile_loop_filter():
         tiles.split(params, pic)
 
 
-def _worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+def _worker(rank, world):
     import hashlib
-    import torch.distributed as tdist
-    tdist.init_process_group("gloo")
     params = R.make_params(pic_width=192, pic_height=128) if rank == 0 else R.make_params()   # ranks disagree...
     params = dist.broadcast_params(params)                                                      # ...until broadcast
     mine = dist.frame_shard(6, rank, world)
@@ -56,25 +52,66 @@ def _worker(rank, world, port, out_dir):
     dig = [(f, hashlib.sha256(b"".join(o[1][c].tobytes() for c in range(3))).hexdigest()) for f, o in zip(mine, outs)]
     merged = dist.gather_digests(dig)
     t = dist.max_over_ranks(float(rank + 1))
-    if rank == 0:
-        np.save(os.path.join(out_dir, "result.npy"), np.array([len(merged), t, int(params["pic_width"])]))
-        import json
-        json.dump(merged, open(os.path.join(out_dir, "digests.json"), "w"))
-    tdist.destroy_process_group()
+    return len(merged), t, int(params["pic_width"]), merged
 
 
-def test_gloo_world2_frame_sharding(tmp_path):
-    import json
-    import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    n, t, width = np.load(tmp_path / "result.npy")
-    assert (n, t, width) == (6, 2.0, 192)
-    merged = json.load(open(tmp_path / "digests.json"))
+def test_world2_frame_sharding_over_the_control_plane():
     import hashlib
+    from ranks import run_ranks
+    res = run_ranks(_worker, 2)
+    for rank in (0, 1):
+        n, t, width, merged = res[rank]
+        assert (n, t, width) == (6, 2.0, 192)
     params = R.make_params(pic_width=192, pic_height=128)
     ref = c_oracle.decode(params, [synth.make_picture(params, 900 + f) for f in range(6)])
     for f in range(6):
-        assert merged[str(f)] == hashlib.sha256(b"".join(ref[f][1][c].tobytes() for c in range(3))).hexdigest()
+        assert res[0][3][f] == hashlib.sha256(b"".join(ref[f][1][c].tobytes() for c in range(3))).hexdigest()
+
+
+def _comm_worker(rank, world):
+    from p265_amd import dist as D
+    from p265_amd.comm import pack_map, unpack_map
+    c = D.group().ctrl
+    got = {}
+    got["bcast"] = c.bcast(b"hello" if rank == 2 else b"", src=2)
+    got["allgather"] = c.allgather(bytes([rank]) * (rank + 1))
+    got["max"] = c.max(float(10 - rank))
+    c.barrier()
+    got["a2a"] = c.alltoall({d: b"%d->%d" % (rank, d) for d in range(world) if d != rank})
+    got["map"] = unpack_map(pack_map({3: b"x", -1: b""}))
+    sends = [((rank + 1) % world, 100 * rank + 1, b"a" * (rank + 1)), ((rank + 2) % world, 100 * rank + 2, b"")]
+    recvs = [((rank - 1) % world, 100 * ((rank - 1) % world) + 1), ((rank - 2) % world, 100 * ((rank - 2) % world) + 2)]
+    got["exchange"] = D.exchange(sends, recvs)
+    return got
+
+
+def test_control_plane_collectives_three_ranks():
+    from ranks import run_ranks
+    res = run_ranks(_comm_worker, 3)
+    for r in range(3):
+        g = res[r]
+        assert g["bcast"] == b"hello"
+        assert g["allgather"] == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
+        assert g["max"] == 10.0
+        assert g["a2a"] == {s: b"%d->%d" % (s, r) for s in range(3) if s != r}
+        assert g["map"] == {3: b"x", -1: b""}
+        p1, p2 = (r - 1) % 3, (r - 2) % 3
+        assert g["exchange"] == {100 * p1 + 1: b"a" * (p1 + 1), 100 * p2 + 2: b""}
+
+
+def test_product_package_has_no_torch():
+    """north_star: the host side calls the HIP kernels through ctypes, no PyTorch."""
+    import glob
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "p265_amd")
+    for f in glob.glob(os.path.join(root, "*.py")):
+        src = open(f).read()
+        assert "import torch" not in src and "from torch" not in src, f
+
+
+def test_rccl_binding_loads():
+    """librccl.so.1 and the HIP runtime bind through ctypes (no device needed for the symbols)."""
+    from p265_amd import rccl
+    h = rccl.lib()
+    for name in ("ncclGetUniqueId", "ncclCommInitRank", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclGroupStart"):
+        assert hasattr(h, name)
+    assert rccl.version() >= 20000

@@ -157,23 +157,27 @@ def test_resident_batch_rerun_is_stable(recon_mod):
             np.testing.assert_array_equal(first[i][c], second[i][c])
 
 
-@pytest.mark.parametrize("prio", ["0", "1", "3"])
-def test_pipelined_batches(recon_mod, prio, monkeypatch):
-    """p265r_set_pipeline: three resident batches on different streams, each run several times
-    back to back with the runs interleaved across streams, every output equals the oracle --
-    intra on the lane itself, on a high-priority twin, or intra + filters on a twin (P265R_PRIO)."""
-    monkeypatch.setenv("P265R_PRIO", prio)
+@pytest.mark.parametrize("sync_first", [True, False])
+def test_pipelined_batches(recon_mod, sync_first):
+    """p265r_set_pipeline: three resident batches on two streams, each run several times back to
+    back with the runs interleaved across streams; every output equals the oracle, whether the
+    host waits for all streams first (ctx.sync) or downloads each batch right after its last run
+    (the download orders itself behind the batch's own stream)."""
     params = R.make_params(pic_width=320, pic_height=192)
     sets = [[synth.make_picture(params, 700 + 10 * k + s, perf=bool(s % 2)) for s in range(3)] for k in range(3)]
     pd = R.params_dict(params)
     with recon_mod.ReconContext(params) as ctx:
         ctx.set_pipeline(2)
         bs = [ctx.upload(p) for p in sets]
-        for _ in range(3):
-            for b in bs:
+        outs = [None] * len(bs)
+        for rep in range(3):
+            for k, b in enumerate(bs):
                 ctx.run(b)
-        ctx.sync()
-        outs = [ctx.download(b) for b in bs]
+                if rep == 2 and not sync_first:
+                    outs[k] = ctx.download(b)
+        if sync_first:
+            ctx.sync()
+            outs = [ctx.download(b) for b in bs]
         for b in bs:
             b.free()
     for k, pics in enumerate(sets):

@@ -4,7 +4,8 @@ Each tile is reconstructed alone, receives from its neighbours the samples withi
 its edges plus the edge CTUs' records (p265_amd/halo.py), and runs the in-loop filters
 on its extended tile; the stitched result must equal whole-picture decoding.  Here the
 filters are the oracle's (the GPU path is tests/test_gpu_parity.py::test_tile_halo_*),
-and the exchange runs over torch.distributed gloo with two ranks.
+and the exchange runs between two rank processes (p265_amd.dist.exchange over the socket
+control plane; RCCL send / recv on the GPU box).
 """
 import os
 
@@ -80,56 +81,37 @@ def test_without_halo_the_tile_border_differs():
     assert (got[0] != ref[0][y0:y1, x0:x1]).any()
 
 
-def _rank_main(rank, world, port, result_q):
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        params, pic = _case(seed=77)
-        grid = halo.TileGrid.from_picture(params, pic)
-        owner = {t: t % world for t in range(grid.n_tiles)}
-        recons = _tile_recons(params, pic)            # (every rank could; each keeps only its own)
-        mine = {}
-        for t in range(grid.n_tiles):
-            if owner[t] == rank:
-                mine[t] = halo.TileData(grid, pic, t)
-                mine[t].recon = recons[t]
-        sends, recvs = [], []
-        for t, d in mine.items():
-            for n in grid.neighbours(t):
-                recvs.append((owner[n], (n, t))) if owner[n] != rank else None
-            for dst_t in range(grid.n_tiles):
-                if t in grid.neighbours(dst_t) and owner[dst_t] != rank:
-                    sends.append((owner[dst_t], (t, dst_t), d.halo_for(dst_t)))
-        tag_key = lambda k: k[0] * 100 + k[1]
-        got = halo.exchange([(d, tag_key(k), b) for d, k, b in sends], [(s, tag_key(k)) for s, k in recvs])
-        outs = {}
-        for t, d in mine.items():
-            payloads = []
-            for n in grid.neighbours(t):
-                payloads.append(mine[n].halo_for(t) if owner[n] == rank else got[tag_key((n, t))])
-            ep, epic, origin, inner = halo.ext_picture(params, grid, d, payloads)
-            outs[t] = halo.crop_inner(_filter_ext(ep, epic), origin, inner)
-        _check_tiles(params, pic, outs, grid)
-        result_q.put((rank, "ok"))
-    except Exception as e:  # pragma: no cover - reported to the parent
-        result_q.put((rank, repr(e)))
-    finally:
-        dist.destroy_process_group()
+def _rank_main(rank, world):
+    params, pic = _case(seed=77)
+    grid = halo.TileGrid.from_picture(params, pic)
+    owner = {t: t % world for t in range(grid.n_tiles)}
+    recons = _tile_recons(params, pic)            # (every rank could; each keeps only its own)
+    mine = {}
+    for t in range(grid.n_tiles):
+        if owner[t] == rank:
+            mine[t] = halo.TileData(grid, pic, t)
+            mine[t].recon = recons[t]
+    sends, recvs = [], []
+    for t, d in mine.items():
+        for n in grid.neighbours(t):
+            if owner[n] != rank:
+                recvs.append((owner[n], (n, t)))
+        for dst_t in range(grid.n_tiles):
+            if t in grid.neighbours(dst_t) and owner[dst_t] != rank:
+                sends.append((owner[dst_t], (t, dst_t), d.halo_for(dst_t)))
+    tag_key = lambda k: k[0] * 100 + k[1]
+    got = halo.exchange([(d, tag_key(k), b) for d, k, b in sends], [(s, tag_key(k)) for s, k in recvs])
+    outs = {}
+    for t, d in mine.items():
+        payloads = []
+        for n in grid.neighbours(t):
+            payloads.append(mine[n].halo_for(t) if owner[n] == rank else got[tag_key((n, t))])
+        ep, epic, origin, inner = halo.ext_picture(params, grid, d, payloads)
+        outs[t] = halo.crop_inner(_filter_ext(ep, epic), origin, inner)
+    _check_tiles(params, pic, outs, grid)
+    return "ok"
 
 
-def test_halo_exchange_gloo_two_ranks():
-    import multiprocessing as mp
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=240) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-    assert res == {0: "ok", 1: "ok"}, res
+def test_halo_exchange_two_ranks():
+    from ranks import run_ranks
+    assert run_ranks(_rank_main, 2) == {0: "ok", 1: "ok"}

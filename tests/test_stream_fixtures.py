@@ -3,13 +3,12 @@
 Each picture of these streams carries an MD5 decoded-picture-hash SEI.  Parsing the bytes
 with the native front-end and reconstructing with the C oracle must reproduce every hash;
 config C5 (4K, 2x2 tiles, 2 pictures) is also decoded tile by tile as independent
-sub-pictures, sharded over a world_size-2 gloo group as the 8-GPU run shards it, and
+sub-pictures, sharded over two rank processes (socket control plane) as the 8-GPU run shards it, and
 stitched back.
 """
 import hashlib
 import json
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -50,11 +49,7 @@ def test_1080p_fixture_has_the_surveyed_statistics():
     assert all(int(p.params["pic_width"]) == 1920 and int(p.params["pic_height"]) == 1080 for p in pics)
 
 
-def _c5_worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    import torch.distributed as tdist
-    tdist.init_process_group("gloo")
+def _c5_worker(rank, world):
     pics = bitstream.decode_stream(_load("synth_4k_tiles.bin"))          # every rank parses the stream
     params = dist.broadcast_params(pics[0].params)
     digests = []
@@ -62,19 +57,12 @@ def _c5_worker(rank, world, port, out_dir):
         tp, tpic, origin = tiles.split(params, pics[f].picture)[t]
         planes = c_oracle.decode(tp, [tpic], with_recon=False)[0][1]
         digests.append(("%d/%d" % (f, t), [np.ascontiguousarray(planes[c]).tobytes().hex() for c in range(3)]))
-    merged = dist.gather_digests(digests)
-    if rank == 0:
-        json.dump(merged, open(os.path.join(out_dir, "tiles.json"), "w"))
-    tdist.destroy_process_group()
+    return dist.gather_digests(digests)
 
 
-def test_c5_tile_units_sharded_over_two_ranks_reproduce_the_md5(tmp_path):
-    import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    mp.spawn(_c5_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    merged = json.load(open(tmp_path / "tiles.json"))
+def test_c5_tile_units_sharded_over_two_ranks_reproduce_the_md5():
+    from ranks import run_ranks
+    merged = run_ranks(_c5_worker, 2)[0]
     pics = bitstream.decode_stream(_load("synth_4k_tiles.bin"))
     assert len(merged) == 8                                               # 2 pictures x 4 tiles
     for f, p in enumerate(pics):

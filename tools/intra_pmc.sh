@@ -3,7 +3,7 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --steps 2 --warmup 1 --frames 512 --unique 2 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-}"
+B="python bench.py --experiment --steps 2 --warmup 1 --frames 512 --unique 2 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-}"
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 P2="SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC"
 P3="SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_ACTIVE_INST_VMEM SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_IFETCH"

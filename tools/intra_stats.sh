@@ -3,7 +3,7 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --steps 2 --warmup 1 --frames 512 --unique 2 --no-cpu-baseline"
+B="python bench.py --experiment --steps 2 --warmup 1 --frames 512 --unique 2 --no-cpu-baseline"
 P265R_DEBUG_SYNC=1 timeout -k 10 300 $B > gpurun_out/intra_dbg.log 2>&1 || true
 grep "dependency waits" gpurun_out/intra_dbg.log | tail -2
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY --output-format csv -d gpurun_out/isq -o sq -- $B > gpurun_out/isq.log 2>&1

@@ -4,7 +4,7 @@ set -e
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_sao
 mkdir -p $OUT
-B="python bench.py --steps 3 --warmup 1 --unique 2 --no-cpu-baseline --no-e2e --pipeline 1"
+B="python bench.py --experiment --steps 3 --warmup 1 --unique 2 --no-cpu-baseline --no-e2e --pipeline 1"
 for v in 1 0; do
 P265R_SAO_ROWS=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt$v -o kt -- $B > $OUT/kt$v.log 2>&1
 P265R_SAO_ROWS=$v timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY --output-format csv -d $OUT/sq$v -o sq -- $B > $OUT/sq$v.log 2>&1
