@@ -189,27 +189,51 @@ class PictureBuilder:
 
 class ReconHook:
     """Adapter for live reference objects (duck-typed), i.e. the lines a maintainer adds
-    to decoder/cu.py:487 (``self.ctx.recon.on_decode_leaf(self)``) and ctu.py:28.
+    to decoder/cu.py:487 (``self.ctx.recon.on_decode_leaf(self)``), ctu.py:28
+    (``self.ctx.recon.on_ctu_parsed(self, self.ctx.img.slice_hdr, self.ctx.pps)``) and
+    slice.py:284-286 (``pic = self.ctx.recon.on_end_of_picture()``).
 
     Reads exactly the attributes Cu.decode_intra / IntraPu / scaling would have read:
-    cu.x/y/log2size/part_mode/intra_pred_mode_y/intra_pred_mode_c/qp_y/qp_cb/qp_cr,
-    cu.cu_transquant_bypass_flag/pcm_flag, and the TU leaves' cbf_*,
-    transform_skip_flag and trans_coeff_level (x-major, tu.py:87-90).
+    cu.x/y/size/log2size/part_mode/intra_pred_mode_y (x-major md_dict)/intra_pred_mode_c/
+    qp_y/qp_cb/qp_cr, cu.cu_transquant_bypass_flag/pcm_flag, and the TU leaves' x/y/log2size/
+    idx, cbf_luma/cbf_cb/cbf_cr, transform_skip_flag and trans_coeff_level (x-major,
+    tu.py:87-90; a luma 4x4 quad's shared chroma pair lives on its blkIdx-3 leaf,
+    tu.py:127-135).  PCM CUs: the reference calls an undefined decode_pcm (cu.py:484-485) and
+    never stores the samples, so the hook reads them under their syntax names (7.3.8.7):
+    ``cu.pcm_sample_luma`` (nCbS^2 values, raster) and ``cu.pcm_sample_chroma`` (Cb then Cr,
+    (nCbS/2)^2 each), at PcmBitDepth, shifted to BitDepth as 8.4.4.1 (pcm_bit_depth_*).
+    ``pcm_loop_filter_disabled``: pcm_loop_filter_disabled_flag of the SPS.
     """
 
-    def __init__(self, params, qp_bd_offset_y=0, qp_bd_offset_c=0):
+    def __init__(self, params, qp_bd_offset_y=0, qp_bd_offset_c=0, pcm_bit_depth_luma=8, pcm_bit_depth_chroma=8,
+                 pcm_loop_filter_disabled=False):
         self.params = params
         self.off_y, self.off_c = qp_bd_offset_y, qp_bd_offset_c
-        self.builder = PictureBuilder(params)
+        self.pcm_shift = (int(params["bit_depth_luma"]) - int(pcm_bit_depth_luma),
+                          int(params["bit_depth_chroma"]) - int(pcm_bit_depth_chroma))
+        self.pcm_lf_disabled = bool(pcm_loop_filter_disabled)
+        self.builder = PictureBuilder(params, pcm_loop_filter_disabled=self.pcm_lf_disabled)
         self.pictures = []
+
+    def _pcm_samples(self, cu):
+        n = int(cu.size)
+        h = n >> 1
+        luma = np.asarray(cu.pcm_sample_luma, np.int64).reshape(n, n) << self.pcm_shift[0]
+        ch = np.asarray(cu.pcm_sample_chroma, np.int64).reshape(2, h, h) << self.pcm_shift[1]
+        return [luma.astype(np.int16), ch[0].astype(np.int16), ch[1].astype(np.int16)]
 
     def on_decode_leaf(self, cu):
         modes = [0, 0, 0, 0]
         pm = int(getattr(cu, "part_mode", 0))
-        if not getattr(cu, "pcm_flag", 0):
-            h = cu.size >> 1
-            for i in range(4 if pm == 1 else 1):
-                modes[i] = int(cu.intra_pred_mode_y[cu.x + h * (i % 2)][cu.y + h * (i // 2)])
+        qps = (cu.qp_y + self.off_y, cu.qp_cb + self.off_c, cu.qp_cr + self.off_c)
+        bypass = bool(getattr(cu, "cu_transquant_bypass_flag", 0))
+        if getattr(cu, "pcm_flag", 0):
+            self.builder.add_cu(cu.x, cu.y, cu.log2size, pm, modes, 0, *qps, [], bypass=bypass, pcm=True,
+                                pcm_samples=self._pcm_samples(cu))
+            return
+        h = cu.size >> 1
+        for i in range(4 if pm == 1 else 1):
+            modes[i] = int(cu.intra_pred_mode_y[cu.x + h * (i % 2)][cu.y + h * (i // 2)])
         tus = []
         if getattr(cu, "tu", None) is not None:
             for leaf in cu.tu.get_leaves():
@@ -219,19 +243,21 @@ class ReconHook:
                                 tskip=[int(tsf[c]) if tsf is not None else 0 for c in range(3)],
                                 coef=[np.asarray(leaf.trans_coeff_level[c]).T for c in range(3)]))
         self.builder.add_cu(cu.x, cu.y, cu.log2size, pm, modes, int(getattr(cu, "intra_pred_mode_c", 0)),
-                            cu.qp_y + self.off_y, cu.qp_cb + self.off_c, cu.qp_cr + self.off_c, tus,
-                            bypass=bool(getattr(cu, "cu_transquant_bypass_flag", 0)))
+                            *qps, tus, bypass=bypass)
 
-    def on_ctu_parsed(self, ctu, slice_hdr):
+    def on_ctu_parsed(self, ctu, slice_hdr, pps=None):
         s = ctu.sao
         on = bool(slice_hdr.slice_sao_luma_flag or slice_hdr.slice_sao_chroma_flag)
+        pps = pps if pps is not None else getattr(slice_hdr, "pps", None)
         # slice_deblocking_filter_disabled_flag is never assigned by the reference (slice.py:170-178
         # reads it); absent an override it is inferred from the PPS (pps.py:122-131)
-        pps = getattr(slice_hdr, "pps", None)
         dbk_off = bool(getattr(slice_hdr, "slice_deblocking_filter_disabled_flag",
                                getattr(pps, "pps_deblocking_filter_disabled_flag", 0)))
+        lf_across = getattr(slice_hdr, "slice_loop_filter_across_slices_enabled_flag",
+                            getattr(pps, "pps_loop_filter_across_slices_enabled_flag", 1))
         self.builder.add_ctu(ctu.addr_rs, slice_addr=getattr(ctu, "slice_addr", 0),
-                             lf_across_slices=bool(getattr(slice_hdr, "slice_loop_filter_across_slices_enabled_flag", 1)),
+                             tile_id=int(getattr(ctu, "tile_id", 0)),
+                             lf_across_slices=bool(lf_across),
                              deblocking=not dbk_off,
                              beta_offset_div2=int(getattr(slice_hdr, "slice_beta_offset_div2",
                                                           getattr(pps, "pps_beta_offset_div2", 0))),
@@ -243,10 +269,10 @@ class ReconHook:
                              sao_band=s.sao_band_position if on else (0, 0, 0),
                              sao_eo=s.sao_eo_class if on else (0, 0, 0))
 
-    def on_end_of_picture(self):
-        pic = self.builder.finish()
+    def on_end_of_picture(self, meta=None):
+        pic = self.builder.finish(meta)
         self.pictures.append(pic)
-        self.builder = PictureBuilder(self.params)
+        self.builder = PictureBuilder(self.params, pcm_loop_filter_disabled=self.pcm_lf_disabled)
         return pic
 
 

@@ -34,6 +34,32 @@ def plane_shapes(params):
     return [(h, w), (h // 2, w // 2), (h // 2, w // 2)]
 
 
+class DecodedPicture:
+    """One decoded picture, served back to the reference's read-back surface.
+
+    ``get_reconstructed_sample(x, y, c_idx)`` has the semantics of Cu.get_reconstructed_sample
+    (decoder/cu.py:617-632): (x, y) in LUMA coordinates for every component (chroma: the
+    sample at (x >> 1, y >> 1) of its plane, cu.py:624-630), returning the reconstruction
+    before the in-loop filters (pu.reconstructed_samples, reconstruction.py:25), which is what
+    intra prediction of later blocks reads.  ``get_output_sample`` returns the decoded
+    (deblocked + SAO) sample that is written out.  ``planes`` / ``recon`` are [Y, Cb, Cr]
+    uint8 arrays indexed [y][x] (the reference's arrays are x-major [x][y])."""
+
+    def __init__(self, planes, recon):
+        self.planes, self.recon = planes, recon
+
+    @staticmethod
+    def _at(planes, x, y, c_idx):
+        sub = 1 if c_idx else 0
+        return int(planes[c_idx][y >> sub, x >> sub])
+
+    def get_reconstructed_sample(self, x, y, c_idx):
+        return self._at(self.recon, x, y, c_idx)
+
+    def get_output_sample(self, x, y, c_idx):
+        return self._at(self.planes, x, y, c_idx)
+
+
 class Batch:
     def __init__(self, ctx, handle, pics, keep):
         self.ctx, self.handle, self.pics, self._keep = ctx, handle, pics, keep
@@ -183,6 +209,13 @@ class ReconContext:
         _lib.check(self.lib.p265r_wait(self.handle), "p265r_wait")
         del keep
         return (outs, recs) if with_recon else outs
+
+
+def decode_pictures(ctx, pics):
+    """ReconContext.decode with the reconstruction too, as DecodedPicture objects (the
+    read-back surface of decoder/cu.py:617-632)."""
+    outs, recs = ctx.decode(pics, with_recon=True)
+    return [DecodedPicture(o, r) for o, r in zip(outs, recs)]
 
 
 def device_count():

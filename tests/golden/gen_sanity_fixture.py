@@ -20,6 +20,13 @@ on each CTU:
 Output: tests/golden/sanity_frontend.npz (data only: inputs of the hot path)
 plus tests/golden/sanity_frontend.json (provenance + golden-match summary).
 
+The same decode also drives the drop-in adapter p265_amd.frontend.ReconHook with the LIVE
+reference objects -- exactly the calls INTEGRATION.md tells a maintainer to add at
+cu.py:487 (on_decode_leaf), ctu.py:28 (on_ctu_parsed) and slice.py:284-286
+(on_end_of_picture) -- and asserts that the records it builds equal, bit for bit, the
+records rebuilt from the committed capture (frontend.pictures_from_frontend_npz).  The npz
+is rewritten only if its arrays changed (zip timestamps would change its hash).
+
 Usage:  PYTHONDONTWRITEBYTECODE=1 python3 -B tests/golden/gen_sanity_fixture.py
 """
 import filecmp
@@ -35,6 +42,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import _refshim  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from p265_amd import frontend  # noqa: E402
+from p265_amd import records as R  # noqa: E402
 
 WORK = "/tmp/p265_sanity_fixture"
 BITSTREAM = os.path.join(_refshim.REF_ROOT, "sanity.bin")
@@ -53,15 +64,29 @@ def main():
     mods = _refshim.install(WORK)
     cu_mod, ctu_mod, slice_mod = mods["cu"], mods["ctu"], mods["slice"]
 
-    state = {"frame": 0}
+    state = {"frame": 0, "hook": None}
     cus, tus, coefs, ctus = [], [], [], []
 
     orig_decode_leaf = cu_mod.Cu.decode_leaf
     orig_ctu_parse = ctu_mod.Ctu.parse
     orig_sd_parse = slice_mod.SliceSegmentData.parse
 
+    def hook(ctx):
+        if state["hook"] is None:                   # created once the SPS / PPS are active
+            sps = ctx.sps
+            prm = R.make_params(pic_width=sps.pic_width_in_luma_samples, pic_height=sps.pic_height_in_luma_samples,
+                                chroma_format_idc=sps.chroma_format_idc, bit_depth_luma=sps.bit_depth_y,
+                                bit_depth_chroma=sps.bit_depth_c, ctb_log2_size=sps.ctb_log2_size_y,
+                                min_tb_log2_size=sps.log2_min_transform_block_size,
+                                max_tb_log2_size=sps.log2_max_transform_block_size,
+                                strong_intra_smoothing=int(sps.strong_intra_smoothing_enabled_flag),
+                                sample_adaptive_offset=int(sps.sample_adaptive_offset_enabled_flag))
+            state["hook"] = frontend.ReconHook(prm, sps.qp_bd_offset_y, sps.qp_bd_offset_c)
+        return state["hook"]
+
     def decode_leaf(self):
         orig_decode_leaf(self)                      # runs decode_qp (cu.py:487)
+        hook(self.ctx).on_decode_leaf(self)         # the maintainer's line at cu.py:487
         root = self.get_root()
         sps = self.ctx.sps
         if self.pred_mode != self.MODE_INTRA:
@@ -98,6 +123,7 @@ def main():
     def ctu_parse(self):
         orig_ctu_parse(self)
         sh = self.ctx.img.slice_hdr
+        hook(self.ctx).on_ctu_parsed(self, sh, self.ctx.pps)      # the maintainer's line at ctu.py:28
         s = self.sao
         sao_on = bool(sh.slice_sao_luma_flag or sh.slice_sao_chroma_flag)
         typ = [int(v) for v in s.sao_type_idx] if sao_on else [0, 0, 0]
@@ -115,6 +141,7 @@ def main():
     def sd_parse(self):
         eop = orig_sd_parse(self)
         if eop:
+            hook(self.ctx).on_end_of_picture({"source": "sanity.bin", "frame": state["frame"]})   # slice.py:284-286
             state["frame"] += 1
         return eop
 
@@ -190,15 +217,41 @@ def main():
 
     cu_a, tu_a, coef_a, ctu_a = pack(cus, cu_dt), pack(tus, tu_dt), pack(coefs, coef_dt), pack(ctus, ctu_dt)
     out = os.path.join(HERE, "sanity_frontend.npz")
-    np.savez_compressed(out, cus=cu_a, tus=tu_a, coefs=coef_a, ctus=ctu_a,
-                        params=np.frombuffer(json.dumps(params).encode(), np.uint8))
+    arrays = dict(cus=cu_a, tus=tu_a, coefs=coef_a, ctus=ctu_a, params=np.frombuffer(json.dumps(params).encode(), np.uint8))
+    same = False
+    if os.path.exists(out):
+        old = np.load(out, allow_pickle=False)
+        same = set(old.files) == set(arrays) and all(np.array_equal(old[k], v) and old[k].dtype == v.dtype
+                                                     for k, v in arrays.items())
+    if not same:
+        np.savez_compressed(out, **arrays)
+    print("capture %s the committed npz" % ("equals" if same else "REWROTE"))
+
+    # the drop-in adapter, driven by the live reference objects, builds the same records
+    _, rebuilt = frontend.pictures_from_frontend_npz(out)
+    hooked = state["hook"].pictures
+    if len(hooked) != len(rebuilt):
+        raise SystemExit("ReconHook built %d pictures, capture %d" % (len(hooked), len(rebuilt)))
+    for i, (a, b) in enumerate(zip(hooked, rebuilt)):
+        for name in ("ctus", "tbs", "coef"):
+            if not np.array_equal(getattr(a, name), getattr(b, name)):
+                raise SystemExit("ReconHook records differ from the capture: picture %d %s" % (i, name))
+        if (a.nofilter is None) != (b.nofilter is None) or (a.nofilter is not None and not np.array_equal(a.nofilter, b.nofilter)):
+            raise SystemExit("ReconHook no-filter map differs: picture %d" % i)
+    print("ReconHook records identical (%d pictures, %d TB records)" % (len(hooked), sum(len(p.tbs) for p in hooked)))
     with open(BITSTREAM, "rb") as f:
         bs_sha = hashlib.sha256(f.read()).hexdigest()
-    meta = dict(generator="tests/golden/gen_sanity_fixture.py", bitstream="reference:sanity.bin",
+    old_meta = {}
+    if os.path.exists(os.path.join(HERE, "sanity_frontend.json")):
+        old_meta = json.load(open(os.path.join(HERE, "sanity_frontend.json")))
+    meta = dict(old_meta)       # keeps fields other scripts add (pin_sanity_yuv.py: decoded-YUV hashes)
+    meta.update(generator="tests/golden/gen_sanity_fixture.py", bitstream="reference:sanity.bin",
                 bitstream_sha256=bs_sha, golden_files_checked=len(golden), golden_files_matching=len(golden),
                 n_frames=state["frame"], n_cus=len(cus), n_tus=len(tus), n_nonzero_coefs=len(coefs),
                 n_ctus=len(ctus), decode_seconds=round(t_dec, 1), params=params,
-                npz_sha256=hashlib.sha256(open(out, "rb").read()).hexdigest())
+                npz_sha256=hashlib.sha256(open(out, "rb").read()).hexdigest(),
+                reconhook_identical=True,
+                reconhook_tb_records=int(sum(len(p.tbs) for p in hooked)))
     with open(os.path.join(HERE, "sanity_frontend.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print(json.dumps(meta, indent=1, sort_keys=True))

@@ -73,6 +73,29 @@ def test_sanity_bin_frames(recon_mod, schedule):
     _check(recon_mod, params, pics, "sanity")
 
 
+def test_sanity_bin_yuv_pinned(recon_mod):
+    """C1 pin: the HIP output of sanity.bin hashes to the committed SHA-256 of the 3-frame I420
+    YUV (tests/golden/pin_sanity_yuv.py) -- conformant (deblocking + SAO), SURVEY §0.7's recon +
+    SAO, and the reconstruction -- independently of the oracle computed in this run."""
+    import hashlib
+    import json
+    pins = json.load(open(os.path.join(GOLDEN, "sanity_frontend.json")))["decoded_yuv_sha256"]
+    params, pics = frontend.pictures_from_frontend_npz(os.path.join(GOLDEN, "sanity_frontend.npz"))
+    _, nodbk = frontend.pictures_from_frontend_npz(os.path.join(GOLDEN, "sanity_frontend.npz"), deblocking=False)
+    with recon_mod.ReconContext(params) as ctx:
+        outs, recs = ctx.decode(pics, with_recon=True)
+        outs_nodbk = ctx.decode(nodbk)
+    def sha(frames):
+        return hashlib.sha256(b"".join(np.ascontiguousarray(p).tobytes() for f in frames for p in f)).hexdigest()
+    assert sha(outs) == pins["conformant"]
+    assert sha(outs_nodbk) == pins["recon_sao"]
+    assert sha(recs) == pins["recon"]
+    with recon_mod.ReconContext(params) as ctx:
+        dp = recon_mod.decode_pictures(ctx, pics[:1])[0]
+    assert dp.get_reconstructed_sample(17, 9, 1) == recs[0][1][4, 8]
+    assert dp.get_output_sample(351, 287, 0) == outs[0][0][287, 351]
+
+
 def test_config2_single_ctu(recon_mod):
     params, pic = synth.c2_picture()
     _check(recon_mod, params, [pic], "c2")
