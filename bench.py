@@ -230,7 +230,10 @@ def end_to_end(device, reps=16, threads=16):
 
 
 def build_workload(a, rank, world):
-    """-> (params of the batch pictures, [pictures of this rank], cpu-baseline sample, config dict)."""
+    """-> ([(params, [pictures of this rank with those params])], cpu-baseline sample, config dict).
+
+    One group for c3.  c5 has two: a uniform 2x2 tiling of 60 x 34 CTBs gives 30 x 17 CTBs per
+    tile, i.e. 1920 x 1088 top tiles and 1920 x 1072 bottom tiles (the picture ends at 2160)."""
     from p265_amd import dist, synth, tiles
     from p265_amd import records as R
     if a.workload == "c3":
@@ -245,7 +248,7 @@ def build_workload(a, rank, world):
                            % ("deblocking + " if a.deblocking else "", a.frames, a.unique),
                "pictures_per_gpu": a.frames, "ctus_per_picture": len(pics[0].ctus), "ctb": 64,
                "parallelism": "picture-sharded x%d (picture f -> rank f mod N)" % world}
-        return params, pics, (uniq, "1080p pictures"), cfg
+        return [(params, pics)], (params, uniq, "1080p pictures"), cfg
     # C5: 4K, uniform 2x2 tiles, loop_filter_across_tiles 0: every (frame, tile) unit is a
     # 1920x1080 sub-picture of its own (p265_amd/tiles.py); units dealt to ranks
     p4k = R.make_params(pic_width=3840, pic_height=2160, loop_filter_across_tiles=0)
@@ -254,25 +257,28 @@ def build_workload(a, rank, world):
               for f in range(a.c5_frames)]
     mine = dist.unit_shard(a.c5_frames, 4, rank, world)
     parts = {f: tiles.split(p4k, frames[f]) for f in sorted({f for f, _ in mine})}
-    pics = []
-    params = None
+    groups = {}
     for f, t in mine:
         tp, tpic, _ = parts[f][t]
-        if params is None:
-            params = tp
-        elif tp.tobytes() != params.tobytes():
-            raise RuntimeError("c5: tile units of unequal size")
         tpic.meta["samples"] = int(tp["pic_width"]) * int(tp["pic_height"]) * 3 // 2
-        pics.append(tpic)
-    if not pics:
+        groups.setdefault(tp.tobytes(), (tp, []))[1].append(tpic)
+    if not groups:
         raise RuntimeError("c5: rank %d has no tile unit (more ranks than units)" % rank)
+    groups = list(groups.values())
+    cols, rows = tiles.tile_grid(p4k, frames[0])
+    ctus_all = a.c5_frames * sum((cols[i + 1] - cols[i]) * (rows[j + 1] - rows[j])
+                                 for i in range(len(cols) - 1) for j in range(len(rows) - 1))
+    pics = [p for _, g in groups for p in g]
+    params = groups[0][0]
     cfg = {"workload": "C5: 4K all-intra + %sSAO (CTU-row SAO kernel), 2x2 uniform tiles x %d frames = %d tile units "
                        "per step over all ranks, %d on this rank" % ("deblocking + " if a.deblocking else "", a.c5_frames,
                                                                      4 * a.c5_frames, len(pics)),
            "pictures_per_gpu": len(pics), "units_per_step": 4 * a.c5_frames,
-           "ctus_per_picture": len(pics[0].ctus), "tile": "%dx%d" % (int(params["pic_width"]), int(params["pic_height"])),
-           "ctb": 64, "parallelism": "(frame, tile) units -> ranks x%d (dist.unit_shard)" % world}
-    return params, pics, (pics, "1920x1080 tile units of 4K frames"), cfg
+           "ctus_per_picture": len(pics[0].ctus),
+           "tiles": sorted({"%dx%d" % (int(tp["pic_width"]), int(tp["pic_height"])) for tp, _ in groups}),
+           "ctus_all_units": ctus_all,
+           "ctb": 64, "parallelism": "(frame, tile) units -> ranks x%d (dist.unit_shard); one context per tile size" % world}
+    return groups, (params, groups[0][1], "%dx%d tile units of 4K frames" % (int(params["pic_width"]), int(params["pic_height"]))), cfg
 
 
 def main():
@@ -293,39 +299,58 @@ def main():
     rank, world, local = dist.init(device=int(os.environ.get("LOCAL_RANK", "0")), rccl=world_env > 1)
 
     t0 = time.time()
-    params, pics, (cpu_sample, cpu_what), cfg = build_workload(a, rank, world)
+    groups, (cpu_params, cpu_sample, cpu_what), cfg = build_workload(a, rank, world)
     gen_s = time.time() - t0
+    pics = [p for _, g in groups for p in g]
 
-    ctx = recon.ReconContext(params, device=local)
-    ctx.set_pipeline(a.pipeline)
-    # one resident batch per stream (same pictures, separate buffers); step k runs batch k % pipeline
-    batches = [ctx.upload(pics) for _ in range(a.pipeline)]
-    n_ctu = len(pics[0].ctus)
+    # one context per picture size (c3: one); each holds one resident batch per stream (same
+    # pictures, separate buffers); step k runs batch k % pipeline of every context
+    ctxs = []
+    for params, gp in groups:
+        ctx = recon.ReconContext(params, device=local)
+        ctx.set_pipeline(a.pipeline)
+        ctxs.append((ctx, [ctx.upload(gp) for _ in range(a.pipeline)]))
+
+    def step(k):
+        for ctx, batches in ctxs:
+            ctx.run(batches[k % a.pipeline])
+
+    def sync_all():
+        for ctx, _ in ctxs:
+            ctx.sync()
+        hip.synchronize()
+
+    n_ctu = sum(len(p.ctus) for p in pics)
     for k in range(a.warmup):
-        ctx.run(batches[k % a.pipeline])
-    ctx.sync()
-    hip.synchronize()
+        step(k)
+    sync_all()
     dist.barrier()
     t_start = time.perf_counter()
     for k in range(a.steps):               # queued back to back, batches alternating over the streams
-        ctx.run(batches[k % a.pipeline])
-    ctx.sync()
-    hip.synchronize()
+        step(k)
+    sync_all()
     elapsed_local = time.perf_counter() - t_start
     dist.barrier()
     elapsed = dist.max_over_ranks(elapsed_local)
-    # phase breakdown + roofline: the same steps on ONE batch (one stream, no overlap), HIP events
-    # around each phase, so every kernel's duration is its own
-    ctx.set_timing(True)
-    for _ in range(a.steps):
-        ctx.run(batches[0])
-    ctx.sync()
-    ctx.set_timing(False)
-    acc = ctx.timings_total()
-    assert acc["runs"] == a.steps
-    knobs = ctx.describe()
+    # phase breakdown + roofline: the same steps on ONE batch per context (one stream, no
+    # overlap, contexts one after another), HIP events around each phase, so every kernel's
+    # duration is its own
+    acc = None
+    for ctx, batches in ctxs:
+        ctx.set_timing(True)
+        for _ in range(a.steps):
+            ctx.run(batches[0])
+        ctx.sync()
+        ctx.set_timing(False)
+        t = ctx.timings_total()
+        assert t["runs"] == a.steps
+        acc = t if acc is None else {k: acc[k] + t[k] for k in acc}
+    knobs = ctxs[0][0].describe()
 
-    total_ctus = (world * len(pics) if a.workload == "c3" else 4 * a.c5_frames) * n_ctu * a.steps
+    if a.workload == "c3":
+        total_ctus = world * n_ctu * a.steps
+    else:                                  # every tile unit of the step, over all ranks
+        total_ctus = cfg["ctus_all_units"] * a.steps
     value = total_ctus / elapsed
     tot_b, intra_b, res_b, sao_b = algorithmic_bytes(pics)
     launches_per_step = acc["intra_launches"] / a.steps
@@ -369,13 +394,14 @@ def main():
         if py_base is not None:
             py_base.update(host_cores_total=host["host_cores_total"], cpu_model=host["cpu_model"])
             out["cpu_baseline"] = py_base
-        cb = cpu_baseline(params, cpu_sample, a.cpu_baseline_seconds, host["cpu_share"], cpu_what)
+        cb = cpu_baseline(cpu_params, cpu_sample, a.cpu_baseline_seconds, host["cpu_share"], cpu_what)
         cb.update(host_cores_total=host["host_cores_total"], cpu_model=host["cpu_model"])
         out["cpu_baseline_c" if py_base is not None else "cpu_baseline"] = cb
     out["host"] = host
-    for b in batches:
-        b.free()
-    ctx.close()
+    for ctx, batches in ctxs:
+        for b in batches:
+            b.free()
+        ctx.close()
     if rank == 0 and world == 1 and not a.no_e2e and a.workload == "c3":
         out["end_to_end"] = end_to_end(local, threads=min(16, host["cpu_share"]))
     if rank == 0:

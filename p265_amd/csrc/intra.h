@@ -43,6 +43,17 @@ struct DevPic {                 // per picture, device-resident table
     uint32_t zero_off;          // residual pool element index of a 256-sample zero block
 };
 
+// Batch-uniform layout of the per-picture arrays (p265r.hip batch_upload places them at fixed
+// strides), so a kernel computes a picture's plane and CTU-record addresses without loading its
+// DevPic first: one dependent memory round trip less
+struct BatchView {
+    uint8_t* rec0;              // picture 0's reconstruction planes (Y at plane_off[0])
+    uint8_t* out0;              // picture 0's output planes (== rec0 without in-loop filters)
+    uint64_t pic_bytes;         // bytes of one picture's three planes
+    uint64_t plane_off[3];      // Y, Cb, Cr offsets inside a picture's planes
+    const p265r_ctu* ctus0;     // picture 0's CTU records (PicSizeInCtbsY per picture)
+};
+
 struct Geo {                    // batch-uniform geometry
     int w, h;                   // luma size
     int cw, ch;                 // chroma size

@@ -185,12 +185,14 @@ __device__ __forceinline__ uint32_t job_w1(int angtab, uint32_t w0, uint32_t w5)
     const int mode = (int)((w0 >> 17) & 63u);
     return (uint32_t)__builtin_amdgcn_ds_bpermute(mode << 2, angtab) | ((w5 & kJ5Bit32) ? 1u << 21 : 0u);
 }
-__global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g) {
+__global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g, BatchView v) {
     __shared__ LumaJobLds sj[kMaxCtuLuma];
     __shared__ ChromaJobLds sc[kMaxCtuChroma];
     __shared__ uint8_t head[kMaxCtuLuma];
     __shared__ uint8_t chead[kMaxCtuChroma];
     const DevPic P = pics[blockIdx.y];
+    // CTU records from the batch layout (no wait for the DevPic load: both in flight together)
+    const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.y * g.wc * g.hc;
     const int addr = blockIdx.x;
     const int lane = threadIdx.x;
     // intraPredAngle | |invAngle| << 8 per mode (256 for the modes without an inverse angle: intra_rows.h ang_inv)
@@ -199,12 +201,12 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const int cx = addr % g.wc, cy = addr / g.wc;
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
-    const p265r_ctu me = P.ctus[addr];
+    const p265r_ctu me = ctus[addr];
     unsigned flags = 0;
-    if (cx > 0 && ctu_same_region(me, P.ctus[addr - 1])) flags |= 1u;
-    if (cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc])) flags |= 2u;
-    if (cx > 0 && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc - 1])) flags |= 4u;
-    if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, P.ctus[addr - g.wc + 1])) flags |= 8u;
+    if (cx > 0 && ctu_same_region(me, ctus[addr - 1])) flags |= 1u;
+    if (cy > 0 && ctu_same_region(me, ctus[addr - g.wc])) flags |= 2u;
+    if (cx > 0 && cy > 0 && ctu_same_region(me, ctus[addr - g.wc - 1])) flags |= 4u;
+    if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, ctus[addr - g.wc + 1])) flags |= 8u;
 
     const p265r_tb* tbs = P.tbs + me.tb_begin;
     IntraJob* jobs = P.jobs + me.tb_begin;

@@ -27,6 +27,7 @@
 #include "loopfilter.h"
 #include "residual.h"
 #include "sao.h"
+#include "sao_ctb.h"
 #include "sao_rows.h"
 #include "tables.h"
 
@@ -90,7 +91,8 @@ struct p265r_ctx {
     int row_waves = 0;         // waves per workgroup of the row pipeline (P265R_ROW_WAVES 4, 6, 8, 10, 12, 16);
                                // 0 = by run: a batch alone 12 (6 per SIMD, 80 VGPRs: lowest latency),
                                // overlapping other lanes' batches 8 register-lean (room beside it)
-    bool sao_rows = true;      // SAO-only batches: streaming SAO kernel (P265R_SAO_ROWS=0: loop-filter kernel)
+    int sao_rows = 1;          // SAO-only batches: 1 per-CTB kernel (CTB 32 / 64; strip kernel for CTB 16),
+                               // 2 strip kernel, 0 loop-filter window kernel (P265R_SAO_ROWS)
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
                                // while other lanes have work queued (P265R_LEAN)
@@ -123,6 +125,7 @@ struct p265r_batch {
     int16_t* d_res = nullptr;
     int* d_err = nullptr;
     ResJob* d_jobs[RC_NUM] = {};
+    BatchView view{};
     int n_jobs[RC_NUM] = {};
     std::vector<DevPic> h_pics;
     hipStream_t stream = nullptr;  // the context lane this batch runs on
@@ -175,6 +178,8 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
             if (c.sao_type[k] == 2 && c.sao_class[k] > 3) return P265R_EINVAL;
             if (c.sao_type[k] == 1 && c.sao_class[k] > 31) return P265R_EINVAL;
         }
+        // Cb and Cr share SaoTypeIdx and SaoEoClass (7.4.9.3.2; sao.py:57-59, 75-77)
+        if (c.sao_type[1] != c.sao_type[2] || (c.sao_type[1] == 2 && c.sao_class[1] != c.sao_class[2])) return P265R_EINVAL;
         const int cx0 = (rs % g.wc) * ctb, cy0 = (rs / g.wc) * ctb;
         int n_luma = 0, n_chroma = 0;
         for (uint32_t i = c.tb_begin; i < c.tb_begin + c.tb_count; ++i) {
@@ -385,7 +390,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
-    if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = v[0] != '0';
+    if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
@@ -634,6 +639,13 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         }
     });
     std::memcpy(host + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
+    b->view.rec0 = dbase + o_rec;
+    b->view.out0 = lf ? dbase + o_out : dbase + o_rec;
+    b->view.pic_bytes = pic_plane_bytes;
+    b->view.plane_off[0] = 0;
+    b->view.plane_off[1] = align_up(plane_bytes[0], 256);
+    b->view.plane_off[2] = b->view.plane_off[1] + align_up(plane_bytes[1], 256);
+    b->view.ctus0 = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus);
     std::memset(host + o_err, 0, o_ctus - o_err);                                        // error word
     // alignment gaps between the arrays: zero, as the device image always had them
     {
@@ -721,7 +733,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (recon && ctx->schedule == 1 && !(skip & 2)) {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
         // of the residuals, timed with the residual phase
-        intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
+        intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g, b->view);
         ++tm.residual_launches;
     }
     if (b->dbk) {
@@ -763,9 +775,19 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
-    if (b->sao && !b->dbk && ctx->sao_rows && !(skip & 4)) {
-        // SAO only: the streaming SAO kernel (sao_rows.h), one wave per (picture, component, CTB
-        // row, 256-sample strip), 4 waves per block, blocks dealt XCD-aware
+    if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && !(skip & 4)) {
+        // SAO only, CTB 32 / 64: one wave per (picture, CTB, luma | Cb + Cr) (sao_ctb.h), 4 waves
+        // per block, blocks dealt XCD-aware
+        const long long waves = 2ll * ctx->n_ctus * b->n_pics;
+        if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
+        const unsigned blocks = (unsigned)((waves + 3) / 4 + 7) / 8 * 8;
+        if (g.ctb_log2 == 6) sao_ctb_kernel<6><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
+        else sao_ctb_kernel<5><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
+        ++tm.sao_launches;
+        HIP_TRY(hipGetLastError());
+    } else if (b->sao && !b->dbk && ctx->sao_rows && !(skip & 4)) {
+        // SAO only, CTB 16 (or P265R_SAO_ROWS=2): the strip kernel (sao_rows.h), one wave per
+        // (picture, component, CTB row, 248-sample strip), 4 waves per block, blocks dealt XCD-aware
         const long long waves = (long long)sao_rows_units(g) * b->n_pics;
         if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
         const long long blocks = (waves + 3) / 4;
@@ -898,7 +920,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "\"pipeline\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, W=8 register-lean while other lanes have work",
-        ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows ? 1 : 0, ctx->skip, ctx->debug_sync ? 1 : 0,
+        ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
         ctx->pipeline, ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG
         1,

@@ -179,6 +179,9 @@ def validate(params, pic: Picture):
         raise RecordError("coefficient range outside coef array")
     if (pic.ctus["sao_type"] > 2).any():
         raise RecordError("bad SaoTypeIdx")
+    st, sc = pic.ctus["sao_type"], pic.ctus["sao_class"]
+    if ((st[:, 1] != st[:, 2]) | ((st[:, 1] == 2) & (sc[:, 1] != sc[:, 2]))).any():
+        raise RecordError("Cb and Cr must share SaoTypeIdx and SaoEoClass (7.4.9.3.2)")
     nib = np.stack([pic.ctus["deblock_offsets"] & 15, pic.ctus["deblock_offsets"] >> 4])
     if ((nib == 7) | (nib == 8) | (nib == 9)).any():
         raise RecordError("deblocking offset_div2 outside -6..6")

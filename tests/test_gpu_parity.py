@@ -51,10 +51,12 @@ ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
                 "rows16": {"P265R_ROW_WAVES": "16", "P265R_LUMA_LEAD": "40"},
                 "rows4": {"P265R_ROW_WAVES": "4", "P265R_QUAD": "1"},
                 "rows_noquad": {"P265R_ROW_WAVES": "8", "P265R_QUAD": "4"},
-                "rows_lf": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "0"}}
+                "rows_lf": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "0"},
+                "rows_saostrip": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "2"}}
 
 
-@pytest.fixture(params=["rows", "rows_auto", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad", "rows_lf"])
+@pytest.fixture(params=["rows", "rows_auto", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad", "rows_lf",
+                        "rows_saostrip"])
 def schedule(request, monkeypatch):
     """Both intra schedules (CU-local row pipeline with 4..16 waves, the register-lean build,
     with and without the luma / chroma 4x4 quad jobs and the Cb+Cr 8x8 fast path; per-diagonal
@@ -244,6 +246,21 @@ def test_invalid_chroma_size_and_tb_count_rejected(recon_mod):
             assert ei.value.code == _lib.EINVAL
 
 
+def test_chroma_sao_type_mismatch_rejected(recon_mod):
+    """Cb and Cr share SaoTypeIdx and SaoEoClass (7.4.9.3.2): records that differ are EINVAL."""
+    from p265_amd import _lib
+    params = R.make_params(pic_width=64, pic_height=64)
+    pic = synth.make_picture(params, 3)
+    for typ, cls in (((0, 2, 1), (0, 0, 0)), ((0, 2, 2), (0, 1, 3))):
+        bad = R.Picture(ctus=pic.ctus.copy(), tbs=pic.tbs, coef=pic.coef)
+        bad.ctus["sao_type"][0] = typ
+        bad.ctus["sao_class"][0] = cls
+        with recon_mod.ReconContext(params) as ctx:
+            with pytest.raises(_lib.P265RError) as ei:
+                ctx.decode([bad])
+            assert ei.value.code == _lib.EINVAL
+
+
 def test_oversized_batch_returns_erange(recon_mod):
     """A batch whose coded coefficients exceed the signed 32-bit residual offsets the row
     kernel uses (2^31 int16) is refused with ERANGE at upload (no device allocation):
@@ -356,12 +373,16 @@ def test_deblocking_4k_tiles(recon_mod):
     _check_c(recon_mod, params, pics, "dbk-4k")
 
 
-def test_sao_only_window_kernel(recon_mod):
-    """SAO-only batches (no deblocking): slices, tiles, bypass, CTB 16/32/64."""
-    for ctb_log2, w, h in ((6, 200, 136), (5, 264, 200), (4, 72, 40)):
+@pytest.mark.parametrize("kernel", ["1", "2"])
+def test_sao_only_window_kernel(recon_mod, kernel, monkeypatch):
+    """SAO-only batches (no deblocking): slices, tiles, bypass, PCM, ragged right / bottom edges
+    (widths not a multiple of 16), CTB 16/32/64, through the per-CTB kernel (P265R_SAO_ROWS=1) and
+    the strip kernel (2)."""
+    monkeypatch.setenv("P265R_SAO_ROWS", kernel)
+    for ctb_log2, w, h in ((6, 200, 136), (5, 264, 200), (4, 72, 40), (6, 136, 72), (5, 328, 104), (6, 1000, 232)):
         params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2, loop_filter_across_tiles=0)
         pics = [synth.make_picture(params, 1700 + s, perf=False, tiles=(2, 1), n_slices=3, lf_across_slices=None,
-                                   bypass_rate=0.05) for s in range(2)]
+                                   bypass_rate=0.05, pcm_rate=0.03 * s) for s in range(2)]
         _check_c(recon_mod, params, pics, "sao-only")
 
 

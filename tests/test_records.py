@@ -116,3 +116,15 @@ def test_synthetic_mix_follows_the_sanity_statistics():
     area = {lg: float(np.sum(luma["log2_size"] == lg) * 4 ** lg / (640 * 384)) for lg in (2, 3, 4, 5)}
     for lg, target in {2: 0.262, 3: 0.307, 4: 0.263, 5: 0.168}.items():
         assert abs(area[lg] - target) < 0.07, (lg, area)
+
+
+def test_chroma_sao_must_share_type_and_class():
+    params = R.make_params(pic_width=64, pic_height=64)
+    pic = synth.make_picture(params, 3)
+    R.validate(params, pic)
+    for typ, cls in (((0, 2, 1), (0, 0, 0)), ((0, 2, 2), (0, 1, 3))):
+        bad = R.Picture(ctus=pic.ctus.copy(), tbs=pic.tbs, coef=pic.coef)
+        bad.ctus["sao_type"][0] = typ
+        bad.ctus["sao_class"][0] = cls
+        with pytest.raises(R.RecordError):
+            R.validate(params, bad)
