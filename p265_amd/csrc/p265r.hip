@@ -778,7 +778,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && !(skip & 4)) {
         // SAO only, CTB 32 / 64: one wave per (picture, CTB, luma | Cb + Cr) (sao_ctb.h), 4 waves
         // per block, blocks dealt XCD-aware
-        const long long waves = 2ll * ctx->n_ctus * b->n_pics;
+        const long long waves = 2ll * ((ctx->n_ctus + P265R_SAO_PAIR - 1) / P265R_SAO_PAIR) * b->n_pics;
         if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
         const unsigned blocks = (unsigned)((waves + 3) / 4 + 7) / 8 * 8;
         if (g.ctb_log2 == 6) sao_ctb_kernel<6><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);

@@ -194,136 +194,170 @@ __device__ __forceinline__ void sao_ctb_rows(const SaoRows<R, NC>& L, uint8_t* _
     }
 }
 
-// One wave: the luma CTB (CHROMA = false) or the Cb + Cr CTBs (CHROMA = true) of CTB rs of picture pic.
+// One CTB of a wave: the luma CTB (CHROMA = false) or the Cb + Cr CTBs (CHROMA = true) of CTB rs of
+// picture pic.  load() issues every memory access the CTB needs (sample rows, CTU records), filter()
+// consumes them, so a wave can put several CTBs' loads in flight before filtering the first.
+template <int L, bool CHROMA>
+struct SaoCtb {
+    using S = SaoCtbShape<L>;
+    static constexpr int NC = CHROMA ? S::NCC : S::NCL, NG = CHROMA ? S::NGC : S::NGL, R = CHROMA ? S::RC : S::RL;
+    static constexpr int sub = CHROMA ? 1 : 0;
+    static constexpr int cs = S::CW >> sub;                        // CTB size in this component
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    SaoRows<R, NC> rows;
+    u4v me0, me1, nb[9];
+    const uint8_t* nf;
+    int rs, bx, by, c, cx, X, y0, W, H, st;
+    bool act;
+    uint64_t pofs;
+
+    __device__ __forceinline__ void load(const DevPic* __restrict__ pics, const Geo& g, const BatchView& v, int pic,
+                                         int rs_, int lane) {
+        rs = rs_;
+        bx = rs % g.wc; by = rs / g.wc;
+        // lane -> (component, column cx, row group ry)
+        const int half = CHROMA ? lane >> 5 : 0;
+        const int hl = CHROMA ? lane & 31 : lane;
+        c = CHROMA ? 1 + half : 0;
+        cx = hl % NC;
+        const int ry = hl / NC;
+        const bool in_layout = ry < NG;
+        W = CHROMA ? g.cw : g.w; H = CHROMA ? g.ch : g.h;
+        X = bx * cs + 16 * cx;
+        y0 = by * cs + R * (in_layout ? ry : 0);
+        act = in_layout && X < W;
+        st = g.stride[c];
+        pofs = (uint64_t)pic * v.pic_bytes + v.plane_off[c];
+        // the sample loads depend on the position only: issued first
+        rows.load(v.rec0 + pofs, st, H, W, X, cx, y0);
+        nf = pics[pic].nofilter;
+        const uint32_t* crec = reinterpret_cast<const uint32_t*>(v.ctus0 + (size_t)pic * g.wc * g.hc);
+        me0 = *reinterpret_cast<const u4v*>(crec + (size_t)rs * 8);
+        me1 = *reinterpret_cast<const u4v*>(crec + (size_t)rs * 8 + 4);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {                             // all nine in flight together
+            const int nx = min(max(bx + k % 3 - 1, 0), g.wc - 1), ny = min(max(by + k / 3 - 1, 0), g.hc - 1);
+            nb[k] = *reinterpret_cast<const u4v*>(crec + (size_t)(ny * g.wc + nx) * 8);
+        }
+    }
+
+    __device__ __forceinline__ void filter(const Geo& g, const BatchView& v) {
+        const int Y0b = by * cs;
+        // ---- the CTB's SAO parameters and 8.7.3.2 permissions of its 3x3 neighbourhood (scalar) ----
+        uint32_t allow = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int dx = k % 3 - 1, dy = k / 3 - 1;
+            const int nx = bx + dx, ny = by + dy;
+            if (nx < 0 || ny < 0 || nx >= g.wc || ny >= g.hc) continue;
+            const int ro = ny * g.wc + nx;
+            const u4v o = nb[k];
+            bool ok = true;
+            const uint32_t ti = me0.y >> 16, to = o.y >> 16;
+            if (o.z != me0.z) {                                   // other slice: the later sample's flag
+                const bool o_first = to < ti || (to == ti && ro < rs);
+                ok = ((o_first ? me0.w : o.w) & P265R_CTU_LF_ACROSS_SLICES) != 0;
+            }
+            if (!g.lf_tiles && to != ti) ok = false;
+            if (ok) allow |= 1u << k;
+        }
+        allow = __builtin_amdgcn_readfirstlane(allow);
+        auto A = [&](int ay, int ax) { return ((allow >> (ay * 3 + ax)) & 1u) != 0; };
+        // record dword 3: flags | SaoTypeIdx[3] << 8; dword 4: class[3] | dbk offsets; 5..7: offsets.
+        // Cb and Cr share SaoTypeIdx and the EO class (validated at upload), not the band position
+        const int typ = (int)((me0.w >> (8 * (c + 1))) & 0xffu);
+        const int cls = (int)((me1.x >> (8 * c)) & 0xffu);
+        const int variant = __builtin_amdgcn_readfirstlane(typ == 0 ? kSaoCopy : (typ == 1 ? kSaoBo : (cls & 3)));
+        const uint32_t o = c == 0 ? me1.y : (c == 1 ? me1.z : me1.w); // SaoOffsetVal[1..4], signed bytes
+        const uint32_t t_lo = typ == 2 ? __builtin_amdgcn_perm(0u, o, 0x020c0100u) : (o << 8);
+        const uint32_t t_hi = o >> 24;
+        const uint32_t n_lo = (t_lo >> 7) & 0x01010101u, n_hi = (t_hi >> 7) & 0x01010101u;
+        const uint32_t tp_lo = t_lo & ~bytes_ff(n_lo), tp_hi = t_hi & ~bytes_ff(n_hi);
+        const uint32_t tn_lo = (~t_lo & bytes_ff(n_lo)) + n_lo, tn_hi = (~t_hi & bytes_ff(n_hi)) + n_hi;
+        const uint32_t bsh = (uint32_t)((32 - cls) & 31);
+        const uint32_t badd = __umul24(bsh, 0x010101u) | bsh << 24;   // (32 - band position) in every byte
+
+        // ---- byte masks: which of the lane's 16 samples may change, per row kind --------------------
+        // neighbour (dx, dy) of sample i of row y is usable iff inside the picture and its CTB allowed;
+        // only sample 0 / 15 can leave the lane's column, only the CTB's first / last row its rows.
+        // Samples at x >= W are stored into the row padding and never read: don't care.
+        const int n_in = W - X;                                    // samples of the lane inside the picture
+        auto col_bits = [&](int dx, int ay) -> uint32_t {          // A-row ay of the neighbour's CTB
+            if (ay < 0) return 0u;                                 // the neighbour's row is outside the picture
+            if (dx == 0) return A(ay, 1) ? 0xffffu : 0u;
+            if (dx < 0) return (A(ay, 1) ? 0xfffeu : 0u) | ((X > 0 && A(ay, cx == 0 ? 0 : 1)) ? 1u : 0u);
+            const uint32_t inner = n_in >= 16 ? 0x7fffu : ((1u << max(n_in - 1, 0)) - 1u);
+            return (A(ay, 1) ? inner : 0u) | ((n_in > 16 && A(ay, cx == NC - 1 ? 2 : 1)) ? 0x8000u : 0u);
+        };
+        const int ylast = min(Y0b + cs, H) - 1;                    // the CTB's last row in the picture
+        // A-row of a vertical neighbour of row y: above (dy = -1) / below (dy = +1); -1 = outside
+        auto row_a = [&](int y, int dy) -> int {
+            if (dy == 0) return 1;
+            if (dy < 0) return y == Y0b ? 0 : 1;                   // Y0b == 0: no CTB row above -> A bits 0
+            return y == ylast ? (y == H - 1 ? -1 : 2) : 1;
+        };
+        auto mask16 = [&](int y) -> uint32_t {
+            if (variant == kSaoCopy) return 0u;
+            if (variant == kSaoBo) return 0xffffu;
+            const int dxa = variant == kSaoEo1 ? 0 : (variant == kSaoEo3 ? 1 : -1);
+            const int dya = variant == kSaoEo0 ? 0 : -1;
+            return col_bits(dxa, row_a(y, dya)) & col_bits(-dxa, row_a(y, -dya));
+        };
+        uint32_t m_first[4], m_mid[4], m_last[4];
+        expand_mask(mask16(y0), m_first);
+        expand_mask(R >= 3 ? mask16(y0 + 1) : 0u, m_mid);          // rows 1 .. R-2
+        expand_mask(mask16(y0 + R - 1), m_last);
+        rows.exchange(cx);
+        uint8_t* dst = v.out0 + pofs;
+        switch (variant) {
+            case kSaoEo0: sao_ctb_rows<kSaoEo0, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+            case kSaoEo1: sao_ctb_rows<kSaoEo1, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+            case kSaoEo2: sao_ctb_rows<kSaoEo2, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+            case kSaoEo3: sao_ctb_rows<kSaoEo3, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+            case kSaoBo:  sao_ctb_rows<kSaoBo, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+            default:      sao_ctb_rows<kSaoCopy, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+        }
+    }
+};
+
+// CTBs per wave (P265R_SAO_PAIR): 2 = two horizontally adjacent CTBs, both loaded before either is
+// filtered (twice the bytes in flight per wave; a luma row pair is one 128-B line)
+#ifndef P265R_SAO_PAIR
+#define P265R_SAO_PAIR 1
+#endif
 template <int L, bool CHROMA>
 __device__ __forceinline__ void sao_ctb_wave(const DevPic* __restrict__ pics, const Geo& g, const BatchView& v,
-                                             int pic, int rs, int lane) {
-    using S = SaoCtbShape<L>;
-    constexpr int NC = CHROMA ? S::NCC : S::NCL, NG = CHROMA ? S::NGC : S::NGL, R = CHROMA ? S::RC : S::RL;
-    constexpr int sub = CHROMA ? 1 : 0;
-    constexpr int cs = S::CW >> sub;                               // CTB size in this component
-    const int bx = rs % g.wc, by = rs / g.wc;
-    // lane -> (component, column cx, row group ry)
-    const int half = CHROMA ? lane >> 5 : 0;
-    const int hl = CHROMA ? lane & 31 : lane;
-    const int c = CHROMA ? 1 + half : 0;
-    const int cx = hl % NC, ry = hl / NC;
-    const bool in_layout = ry < NG;
-    const int W = CHROMA ? g.cw : g.w, H = CHROMA ? g.ch : g.h;
-    const int X0b = bx * cs, Y0b = by * cs;
-    const int X = X0b + 16 * cx;
-    const int y0 = Y0b + R * (in_layout ? ry : 0);
-    const bool act = in_layout && X < W;
-    const int st = g.stride[c];
-    const uint64_t pofs = (uint64_t)pic * v.pic_bytes + v.plane_off[c];
-    // ---- first: the sample loads (position only; no record needed) ----------------------------
-    SaoRows<R, NC> rows;
-    rows.load(v.rec0 + pofs, st, H, W, X, cx, y0);
-    const uint8_t* nf = pics[pic].nofilter;
-
-    // ---- the CTB's SAO parameters and 8.7.3.2 permissions of its 3x3 neighbourhood (scalar) ----
-    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    const uint32_t* crec = reinterpret_cast<const uint32_t*>(v.ctus0 + (size_t)pic * g.wc * g.hc);
-    const u4v me0 = *reinterpret_cast<const u4v*>(crec + (size_t)rs * 8);
-    const u4v me1 = *reinterpret_cast<const u4v*>(crec + (size_t)rs * 8 + 4);
-    u4v nb[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {                                 // all nine in flight together
-        const int nx = min(max(bx + k % 3 - 1, 0), g.wc - 1), ny = min(max(by + k / 3 - 1, 0), g.hc - 1);
-        nb[k] = *reinterpret_cast<const u4v*>(crec + (size_t)(ny * g.wc + nx) * 8);
-    }
-    uint32_t allow = 0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const int dx = k % 3 - 1, dy = k / 3 - 1;
-        const int nx = bx + dx, ny = by + dy;
-        if (nx < 0 || ny < 0 || nx >= g.wc || ny >= g.hc) continue;
-        const int ro = ny * g.wc + nx;
-        const u4v o = nb[k];
-        bool ok = true;
-        const uint32_t ti = me0.y >> 16, to = o.y >> 16;
-        if (o.z != me0.z) {                                       // other slice: the later sample's flag
-            const bool o_first = to < ti || (to == ti && ro < rs);
-            ok = ((o_first ? me0.w : o.w) & P265R_CTU_LF_ACROSS_SLICES) != 0;
-        }
-        if (!g.lf_tiles && to != ti) ok = false;
-        if (ok) allow |= 1u << k;
-    }
-    allow = __builtin_amdgcn_readfirstlane(allow);
-    auto A = [&](int ay, int ax) { return ((allow >> (ay * 3 + ax)) & 1u) != 0; };
-    // record dword 3: flags | SaoTypeIdx[3] << 8; dword 4: class[3] | dbk offsets; 5..7: offsets.
-    // Cb and Cr share SaoTypeIdx and the EO class (validated at upload), not the band position
-    const int typ = (int)((me0.w >> (8 * (c + 1))) & 0xffu);
-    const int cls = (int)((me1.x >> (8 * c)) & 0xffu);
-    const int variant = __builtin_amdgcn_readfirstlane(typ == 0 ? kSaoCopy : (typ == 1 ? kSaoBo : (cls & 3)));
-    const uint32_t o = c == 0 ? me1.y : (c == 1 ? me1.z : me1.w); // SaoOffsetVal[1..4], signed bytes
-    const uint32_t t_lo = typ == 2 ? __builtin_amdgcn_perm(0u, o, 0x020c0100u) : (o << 8);
-    const uint32_t t_hi = o >> 24;
-    const uint32_t n_lo = (t_lo >> 7) & 0x01010101u, n_hi = (t_hi >> 7) & 0x01010101u;
-    const uint32_t tp_lo = t_lo & ~bytes_ff(n_lo), tp_hi = t_hi & ~bytes_ff(n_hi);
-    const uint32_t tn_lo = (~t_lo & bytes_ff(n_lo)) + n_lo, tn_hi = (~t_hi & bytes_ff(n_hi)) + n_hi;
-    const uint32_t bsh = (uint32_t)((32 - cls) & 31);
-    const uint32_t badd = __umul24(bsh, 0x010101u) | bsh << 24;   // (32 - band position) in every byte
-
-    // ---- byte masks: which of the lane's 16 samples may change, per row kind --------------------
-    // neighbour (dx, dy) of sample i of row y is usable iff inside the picture and its CTB allowed;
-    // only sample 0 / 15 can leave the lane's column, only the CTB's first / last row its rows.
-    // Samples at x >= W are stored into the row padding and never read: don't care.
-    const int n_in = W - X;                                        // samples of the lane inside the picture
-    auto col_bits = [&](int dx, int ay) -> uint32_t {              // A-row ay of the neighbour's CTB
-        if (ay < 0) return 0u;                                     // the neighbour's row is outside the picture
-        if (dx == 0) return A(ay, 1) ? 0xffffu : 0u;
-        if (dx < 0) return (A(ay, 1) ? 0xfffeu : 0u) | ((X > 0 && A(ay, cx == 0 ? 0 : 1)) ? 1u : 0u);
-        const uint32_t inner = n_in >= 16 ? 0x7fffu : ((1u << max(n_in - 1, 0)) - 1u);
-        return (A(ay, 1) ? inner : 0u) | ((n_in > 16 && A(ay, cx == NC - 1 ? 2 : 1)) ? 0x8000u : 0u);
-    };
-    const int ylast = min(Y0b + cs, H) - 1;                        // the CTB's last row in the picture
-    // A-row of a vertical neighbour of row y: above (dy = -1) / below (dy = +1); -1 = outside
-    auto row_a = [&](int y, int dy) -> int {
-        if (dy == 0) return 1;
-        if (dy < 0) return y == Y0b ? 0 : 1;                       // Y0b == 0: no CTB row above -> A bits 0
-        return y == ylast ? (y == H - 1 ? -1 : 2) : 1;
-    };
-    auto mask16 = [&](int y) -> uint32_t {
-        if (variant == kSaoCopy) return 0u;
-        if (variant == kSaoBo) return 0xffffu;
-        const int dxa = variant == kSaoEo1 ? 0 : (variant == kSaoEo3 ? 1 : -1);
-        const int dya = variant == kSaoEo0 ? 0 : -1;
-        return col_bits(dxa, row_a(y, dya)) & col_bits(-dxa, row_a(y, -dya));
-    };
-    uint32_t m_first[4], m_mid[4], m_last[4];
-    expand_mask(mask16(y0), m_first);
-    expand_mask(R >= 3 ? mask16(y0 + 1) : 0u, m_mid);              // rows 1 .. R-2
-    expand_mask(mask16(y0 + R - 1), m_last);
-    rows.exchange(cx);
-    uint8_t* dst = v.out0 + pofs;
-    switch (variant) {
-        case kSaoEo0: sao_ctb_rows<kSaoEo0, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
-        case kSaoEo1: sao_ctb_rows<kSaoEo1, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
-        case kSaoEo2: sao_ctb_rows<kSaoEo2, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
-        case kSaoEo3: sao_ctb_rows<kSaoEo3, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
-        case kSaoBo:  sao_ctb_rows<kSaoBo, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
-        default:      sao_ctb_rows<kSaoCopy, R, NC>(rows, dst, st, H, X, y0, act, m_first, m_mid, m_last, tp_lo, tp_hi, tn_lo, tn_hi, badd, nf, g.nf_w, sub); break;
+                                             int pic, int u, int lane) {
+    const int nctb = g.wc * g.hc;
+    if constexpr (P265R_SAO_PAIR == 2) {
+        SaoCtb<L, CHROMA> a, b;
+        const bool two = 2 * u + 1 < nctb;                        // wave-uniform
+        a.load(pics, g, v, pic, 2 * u, lane);
+        if (two) b.load(pics, g, v, pic, 2 * u + 1, lane);
+        a.filter(g, v);
+        if (two) b.filter(g, v);
+    } else {
+        SaoCtb<L, CHROMA> a;
+        a.load(pics, g, v, pic, u, lane);
+        a.filter(g, v);
     }
 }
 
-// grid: 4 waves per block, one wave per (picture, CTB, luma | chroma), XCD-aware block order
-// (each XCD walks a contiguous range of units, so the halo rows CTBs share come from its L2)
 #ifndef P265R_SAO_WPE
 #define P265R_SAO_WPE 4
 #endif
 template <int L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_WPE))) void sao_ctb_kernel(const DevPic* __restrict__ pics, Geo g, BatchView v, int n_pics) {
     const int lane = threadIdx.x & 63;
-    const int nctb = g.wc * g.hc;
-    const int total = 2 * nctb * n_pics;
+    const int per = (g.wc * g.hc + P265R_SAO_PAIR - 1) / P265R_SAO_PAIR;   // waves per component and picture
+    const int total = 2 * per * n_pics;
     const int nblk = (total + 3) >> 2;
     const int bunit = xcd_unit(blockIdx.x, nblk);
     const int unit = __builtin_amdgcn_readfirstlane(bunit * 4 + (int)(threadIdx.x >> 6));
     if (bunit >= nblk || unit >= total) return;                   // whole wave (no barriers)
-    const int pic = unit / (2 * nctb);
-    const int u = unit - pic * 2 * nctb;
-    if (u >= nctb) sao_ctb_wave<L, true>(pics, g, v, pic, u - nctb, lane);
+    const int pic = unit / (2 * per);
+    const int u = unit - pic * 2 * per;
+    if (u >= per) sao_ctb_wave<L, true>(pics, g, v, pic, u - per, lane);
     else sao_ctb_wave<L, false>(pics, g, v, pic, u, lane);
 }
 

@@ -3,7 +3,7 @@
 #   tools/isa.sh [out.s] [extra hipcc flags...]
 out=${1:-/tmp/isa/p265r.s}; shift || true
 mkdir -p "$(dirname "$out")"
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only -S "$@" -o "$out" p265_amd/csrc/p265r.hip || exit 1
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -structurizecfg-skip-uniform-regions=true --cuda-device-only -S "$@" -o "$out" p265_amd/csrc/p265r.hip || exit 1
 python3 - "$out" <<'PY'
 import re, sys
 txt = open(sys.argv[1]).read()
