@@ -288,9 +288,10 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                     int f = R0[k];
                     if (k > 0 && k < 4 * n) {
                         if (strong) {
+                            // (24-bit multiplies: every factor < 2^8; v_mul_lo_u32 is quarter rate)
                             f = k == 2 * n ? corner
-                              : (k < 2 * n ? ((63 - (2 * n - 1 - k)) * corner + (2 * n - k) * bl + 32) >> 6
-                                           : ((63 - (k - 2 * n - 1)) * corner + (k - 2 * n) * tr + 32) >> 6);
+                              : (k < 2 * n ? (__mul24(63 - (2 * n - 1 - k), corner) + __mul24(2 * n - k, bl) + 32) >> 6
+                                           : (__mul24(63 - (k - 2 * n - 1), corner) + __mul24(k - 2 * n, tr) + 32) >> 6);
                         } else {
                             f = ((int)R0[k - 1] + 2 * f + (int)R0[k + 1] + 2) >> 2;
                         }
@@ -308,7 +309,8 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 #pragma unroll
             for (int i = 0; i < S; ++i) {
                 const int x = sx + i;
-                put(i, ((n - 1 - x) * ly + (x + 1) * trs + (n - 1 - sy) * R[2 * n + 1 + x] + (sy + 1) * bls + n) >> (LOG2 + 1));
+                put(i, (__mul24(n - 1 - x, ly) + __mul24(x + 1, trs) + __mul24(n - 1 - sy, (int)R[2 * n + 1 + x]) +
+                        __mul24(sy + 1, bls) + n) >> (LOG2 + 1));
             }
         } else if (mode == 1) {
             const int dc = (wave_sum<PAIR>(dcs, half) + n) >> (LOG2 + 1);
@@ -328,7 +330,8 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
             const int ang = (int)(int8_t)(w1 & 0xffu);
             const int ia = ang_inv(w1);
             if (mode >= 18) {                                        // vertical family
-                const int idx = ((sy + 1) * ang) >> 5, fact = ((sy + 1) * ang) & 31;
+                const int pa = __mul24(sy + 1, ang);
+                const int idx = pa >> 5, fact = pa & 31;
                 auto refk = [&](int r) { return ang_ref<2 * n>(-r, ia, -1); };
                 const bool bflt = !PAIR && n < 32 && mode == 26;
 #pragma unroll
@@ -336,7 +339,7 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                     const int x = sx + i;
                     const int r0 = x + idx + 1;
                     int v = R[refk(r0)];
-                    v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;   // fact = 0: v
+                    v = (__mul24(32 - fact, v) + __mul24(fact, (int)R[refk(r0 + 1)]) + 16) >> 5;   // fact = 0: v
                     if (bflt && x == 0) v = clip_pel((int)R[2 * n + 1] + (((int)R[2 * n - 1 - sy] - (int)R[2 * n]) >> 1), maxv);
                     put(i, v);
                 }
@@ -346,10 +349,11 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 #pragma unroll
                 for (int i = 0; i < S; ++i) {
                     const int x = sx + i;
-                    const int idx = ((x + 1) * ang) >> 5, fact = ((x + 1) * ang) & 31;
+                    const int pa = __mul24(x + 1, ang);
+                    const int idx = pa >> 5, fact = pa & 31;
                     const int r0 = sy + idx + 1;
                     int v = R[refk(r0)];
-                    v = ((32 - fact) * v + fact * (int)R[refk(r0 + 1)] + 16) >> 5;   // fact = 0: v
+                    v = (__mul24(32 - fact, v) + __mul24(fact, (int)R[refk(r0 + 1)]) + 16) >> 5;   // fact = 0: v
                     if (bflt) v = clip_pel((int)R[2 * n - 1] + (((int)R[2 * n + 1 + x] - (int)R[2 * n]) >> 1), maxv);
                     put(i, v);
                 }

@@ -27,7 +27,7 @@
 #include "loopfilter.h"
 #include "residual.h"
 #include "sao.h"
-#include "sao_ctb.h"
+#include "sao_strip16.h"
 #include "sao_rows.h"
 #include "tables.h"
 
@@ -91,8 +91,8 @@ struct p265r_ctx {
     int row_waves = 0;         // waves per workgroup of the row pipeline (P265R_ROW_WAVES 4, 6, 8, 10, 12, 16);
                                // 0 = by run: a batch alone 12 (6 per SIMD, 80 VGPRs: lowest latency),
                                // overlapping other lanes' batches 8 register-lean (room beside it)
-    int sao_rows = 1;          // SAO-only batches: 1 per-CTB kernel (CTB 32 / 64; strip kernel for CTB 16),
-                               // 2 strip kernel, 0 loop-filter window kernel (P265R_SAO_ROWS)
+    int sao_rows = 1;          // SAO-only batches: 1 16-B strip kernel (CTB 32 / 64; 4-B strip kernel for
+                               // CTB 16), 2 4-B strip kernel, 0 loop-filter window kernel (P265R_SAO_ROWS)
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
                                // while other lanes have work queued (P265R_LEAN)
@@ -776,13 +776,13 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
     if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && !(skip & 4)) {
-        // SAO only, CTB 32 / 64: one wave per (picture, CTB, luma | Cb + Cr) (sao_ctb.h), 4 waves
-        // per block, blocks dealt XCD-aware
-        const long long waves = 2ll * ((ctx->n_ctus + P265R_SAO_PAIR - 1) / P265R_SAO_PAIR) * b->n_pics;
+        // SAO only, CTB 32 / 64: the 16-samples-per-lane strip kernel (sao_strip16.h), one wave per
+        // (picture, CTB row, component, 992-sample strip), 4 waves per block, blocks dealt XCD-aware
+        const long long waves = (long long)sao16_units(g) * b->n_pics;
         if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
         const unsigned blocks = (unsigned)((waves + 3) / 4 + 7) / 8 * 8;
-        if (g.ctb_log2 == 6) sao_ctb_kernel<6><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
-        else sao_ctb_kernel<5><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
+        if (g.ctb_log2 == 6) sao_strip16_kernel<6><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
+        else sao_strip16_kernel<5><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
     } else if (b->sao && !b->dbk && ctx->sao_rows && !(skip & 4)) {
