@@ -73,6 +73,9 @@ struct Geo {                    // batch-uniform geometry
 
 __constant__ int8_t  c_angle[35];
 __constant__ int16_t c_inv_angle[35];
+// job word w1 of mode m (intra_prep.h): intraPredAngle (int8) | |invAngle| << 8 (256 for the modes
+// without an inverse angle: intra_rows.h ang_inv)
+__constant__ uint32_t c_angw[35];
 
 __host__ __device__ __forceinline__ int morton4(int x, int y) {      // 4-bit x, y -> 8-bit z-order
     x = (x | (x << 2)) & 0x33; x = (x | (x << 1)) & 0x55;
@@ -134,29 +137,28 @@ __host__ __device__ __forceinline__ bool nb_available_wh(int xl, int yl, int xc,
 // units; only the picture's bottom / right edges cut them unit by unit.
 __host__ __device__ __forceinline__ unsigned long long ref_avail_mask(int c, int xr, int yr, int n, int x0, int y0,
                                                                       int w, int h, int ctb, unsigned flags) {
+    // straight-line form (selects, no branches): the prep kernel evaluates it on every lane at once
     const int sub = c ? 1 : 0;
     const int xc = xr << sub, yc = yr << sub, nl = n << sub;      // luma, CTB-relative
     const int L = (2 * n) >> (c ? 1 : 2);                         // units per side
     const int half = L >> 1;
     const int zc = morton4(xc >> 2, yc >> 2);
-    const bool left = xc > 0 || (flags & 1u);
-    const bool bl = yc + nl < ctb && (xc == 0 ? (flags & 1u) != 0 : morton4((xc - 1) >> 2, (yc + nl) >> 2) < zc);
-    const bool corner = xc > 0 ? (yc > 0 ? true : (flags & 2u) != 0) : (yc > 0 ? (flags & 1u) != 0 : (flags & 4u) != 0);
-    const bool top = yc > 0 || (flags & 2u);
-    const bool tr = xc + nl < ctb ? (yc > 0 ? morton4((xc + nl) >> 2, (yc - 1) >> 2) < zc : (flags & 2u) != 0)
-                                  : (yc == 0 && (flags & 8u));
-    auto bits = [](int lo, int hi) -> unsigned long long {        // bits [lo, hi)
-        return hi <= lo ? 0ull : (((hi >= 64) ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull));
-    };
+    const bool fl = (flags & 1u) != 0, ft = (flags & 2u) != 0, ftl = (flags & 4u) != 0, ftr = (flags & 8u) != 0;
+    const bool left = xc > 0 || fl;
+    const int zbl = morton4(max(xc - 1, 0) >> 2, min(yc + nl, ctb - 1) >> 2);
+    const bool bl = yc + nl < ctb && (xc == 0 ? fl : zbl < zc);
+    const bool corner = xc > 0 ? (yc > 0 || ft) : (yc > 0 ? fl : ftl);
+    const bool top = yc > 0 || ft;
+    const int ztr = morton4(min(xc + nl, ctb - 1) >> 2, max(yc - 1, 0) >> 2);
+    const bool tr = xc + nl < ctb ? (yc > 0 ? ztr < zc : ft) : (yc == 0 && ftr);
+    // bits [lo, hi) for 0 <= lo, hi <= 33 (empty when hi <= lo)
+    auto bits = [](int lo, int hi) -> unsigned long long { return ((1ull << hi) - 1ull) & ~((1ull << lo) - 1ull); };
     const int u_min = max(0, (y0 + yc + 2 * nl - h) >> 2);        // units below the picture: u < u_min
     const int j_max = (w - x0 - xc) >> 2;                          // top units inside the picture: j < j_max
-    unsigned long long m = 0;
-    if (bl) m |= bits(u_min, half);
-    if (left) m |= bits(half, L);
-    if (corner) m |= 1ull << L;
-    if (top) m |= bits(L + 1, L + 1 + half);
-    if (tr) m |= bits(L + 1 + half, L + 1 + min(L, j_max));
-    return m;
+    const unsigned long long m_bl = bits(min(u_min, half), half), m_l = bits(half, L), m_c = 1ull << L;
+    const unsigned long long m_t = bits(L + 1, L + 1 + half);
+    const unsigned long long m_tr = bits(L + 1 + half, L + 1 + max(half, min(L, j_max)));
+    return (bl ? m_bl : 0ull) | (left ? m_l : 0ull) | (corner ? m_c : 0ull) | (top ? m_t : 0ull) | (tr ? m_tr : 0ull);
 }
 
 __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict__ pics,

@@ -179,34 +179,42 @@ __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_
     J.w[4] = zero_off; J.w[5] = l.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
     return J;
 }
-// job word w1 of a staged job: intraPredAngle | |invAngle| << 8 (lane m of angtab holds mode m's; 256 without one),
-// availability bit 32 << 21.  ds_bpermute: call with every lane active.
-__device__ __forceinline__ uint32_t job_w1(int angtab, uint32_t w0, uint32_t w5) {
-    const int mode = (int)((w0 >> 17) & 63u);
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(mode << 2, angtab) | ((w5 & kJ5Bit32) ? 1u << 21 : 0u);
+// job word w1 of a staged job: intraPredAngle | |invAngle| << 8 (c_angw), availability bit 32 << 21
+__device__ __forceinline__ uint32_t job_w1(uint32_t w0, uint32_t w5) {
+    return c_angw[(w0 >> 17) & 63u] | ((w5 & kJ5Bit32) ? 1u << 21 : 0u);
 }
+// grid (wc, hc, pictures), one 64-thread wave per CTU
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g, BatchView v) {
     __shared__ LumaJobLds sj[kMaxCtuLuma];
     __shared__ ChromaJobLds sc[kMaxCtuChroma];
     __shared__ uint8_t head[kMaxCtuLuma];
     __shared__ uint8_t chead[kMaxCtuChroma];
-    const DevPic P = pics[blockIdx.y];
+    __shared__ uint32_t cq_base[kMaxCtuChroma], cq_codes[kMaxCtuChroma];   // chroma quads found at detection
+    const DevPic P = pics[blockIdx.z];
     // CTU records from the batch layout (no wait for the DevPic load: both in flight together)
-    const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.y * g.wc * g.hc;
-    const int addr = blockIdx.x;
+    const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.z * g.wc * g.hc;
+    const int cx = blockIdx.x, cy = blockIdx.y;
+    const int addr = cy * g.wc + cx;
     const int lane = threadIdx.x;
-    // intraPredAngle | |invAngle| << 8 per mode (256 for the modes without an inverse angle: intra_rows.h ang_inv)
-    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)(int8_t)kIntraPredAngle[lane] |
-                                         (uint32_t)(kInvAngle[lane] ? -kInvAngle[lane] : 256) << 8) : 0;
-    const int cx = addr % g.wc, cy = addr / g.wc;
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
-    const p265r_ctu me = ctus[addr];
+    // this CTU's record and its left / top / top-left / top-right neighbours' first 16 B (slice,
+    // tile), all five loads in flight together (clamped addresses, used only where they exist)
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    const u4v* cr = reinterpret_cast<const u4v*>(ctus);
+    const u4v me4 = cr[2 * addr];
+    const int al = cx > 0 ? addr - 1 : addr, at = cy > 0 ? addr - g.wc : addr;
+    const int atl = (cx > 0 && cy > 0) ? addr - g.wc - 1 : addr, atr = (cx + 1 < g.wc && cy > 0) ? addr - g.wc + 1 : addr;
+    const u4v nl = cr[2 * al], nt = cr[2 * at], ntl = cr[2 * atl], ntr = cr[2 * atr];
+    // dword 1: tb_count | tile_id << 16; dword 2: slice_addr
+    auto same = [&](const u4v& o) { return o.z == me4.z && (o.y >> 16) == (me4.y >> 16); };
     unsigned flags = 0;
-    if (cx > 0 && ctu_same_region(me, ctus[addr - 1])) flags |= 1u;
-    if (cy > 0 && ctu_same_region(me, ctus[addr - g.wc])) flags |= 2u;
-    if (cx > 0 && cy > 0 && ctu_same_region(me, ctus[addr - g.wc - 1])) flags |= 4u;
-    if (cx + 1 < g.wc && cy > 0 && ctu_same_region(me, ctus[addr - g.wc + 1])) flags |= 8u;
+    if (cx > 0 && same(nl)) flags |= 1u;
+    if (cy > 0 && same(nt)) flags |= 2u;
+    if (cx > 0 && cy > 0 && same(ntl)) flags |= 4u;
+    if (cx + 1 < g.wc && cy > 0 && same(ntr)) flags |= 8u;
+    p265r_ctu me;
+    __builtin_memcpy(&me, &me4, 16);
 
     const p265r_tb* tbs = P.tbs + me.tb_begin;
     IntraJob* jobs = P.jobs + me.tb_begin;
@@ -263,11 +271,13 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const int slot = kl ? out_l + rank(ml) : out_c + rank(mc);
         out_l += __popcll(ml);
         out_c += __popcll(mc);
-        if (keep) {
-            const int lg = rec.log2_size, n = 1 << lg, c = rec.c_idx;
+        // every lane computes its job record (straight-line, selects only; lanes without a TB use
+        // a 4x4 luma stand-in), only the kept ones store it: no divergent branches in the chunk
+        {
+            const int lg = max((int)rec.log2_size, 2), n = 1 << lg, c = rec.c_idx;
             const int sub = c ? 1 : 0;
             const bool pair = c == 1 && t + 1 < cnt && tb_same_tu_chroma(rec, next);
-            const int xr = rec.x - (x0 >> sub), yr = rec.y - (y0 >> sub);
+            const int xr = (int)rec.x - (x0 >> sub), yr = (int)rec.y - (y0 >> sub);
             const uint32_t ofs = c == 0 ? (uint32_t)(yr * 64 + xr) : (uint32_t)(4096 + yr * 32 + xr);
             const uint32_t cm = c == 0 ? 0u : (pair ? 3u : (uint32_t)c);
             const int mode = rec.pred_mode;
@@ -276,11 +286,9 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const unsigned long long m = ref_avail_mask(c, xr, yr, n, x0, y0, g.w, g.h, ctb, flags);
             const unsigned long long full = (1ull << (2 * L + 1)) - 1ull;
             // ---- filtering decision (8.4.4.2.3), luma only in 4:2:0 ---------------------------
-            uint32_t filt = 0;
-            if (c == 0 && n != 4 && mode != 1) {
-                const int dist = min(abs(mode - 26), abs(mode - 10));
-                if (dist > (n == 8 ? 7 : (n == 16 ? 1 : 0))) filt = (n == 32 && g.strong) ? 2u : 1u;
-            }
+            const int dist = min(abs(mode - 26), abs(mode - 10));
+            const bool fon = c == 0 && n != 4 && mode != 1 && dist > (n == 8 ? 7 : (n == 16 ? 1 : 0));
+            const uint32_t filt = fon ? ((n == 32 && g.strong) ? 2u : 1u) : 0u;
             const uint32_t f0 = rec.flags;
             const uint32_t f1 = pair ? next.flags : 0u;
             // half 0 = luma / Cb, half 1 = Cr (an unpaired Cr TB lives in half 1)
@@ -290,42 +298,30 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             auto roff = [&](uint32_t f, uint32_t off) {
                 return !coded(f) ? P.zero_off : (raw(f) ? off + (uint32_t)P.pool_rel : off);
             };
-            const uint32_t off0 = cm == 2 ? P.zero_off : roff(f0, rec.coef_off);
-            const uint32_t off1 = cm == 2 ? roff(f0, rec.coef_off) : (pair ? roff(f1, next.coef_off) : P.zero_off);
-            IntraJob J;
-            J.w[0] = ofs | (uint32_t)(lg - 2) << 13 | cm << 15 | (uint32_t)mode << 17 |
-                     ((f0 & P265R_TB_PCM) ? J_PCM : 0u) | filt << 24 | raw(fh0) << 26 | raw(fh1) << 27 |
-                     coded(fh0) << 28 | coded(fh1) << 29 | (m == full ? J_ALL : 0u) | (m == 0 ? J_NONE : 0u);
-            J.w[1] = (uint32_t)(uint8_t)(int8_t)kIntraPredAngle[mode] | (uint32_t)(-kInvAngle[mode]) << 8 |
-                     (uint32_t)((m >> 32) & 1ull) << 21;
-            J.w[2] = (uint32_t)m;
-            J.w[3] = off0;
-            J.w[4] = off1;
-            // fast path: one contiguous run of available units -> sample bounds [fa, la]
-            uint32_t w5 = 0;
+            const uint32_t r0 = roff(f0, rec.coef_off);
+            const uint32_t off0 = cm == 2 ? P.zero_off : r0;
+            const uint32_t off1 = cm == 2 ? r0 : (pair ? roff(f1, next.coef_off) : P.zero_off);
+            const uint32_t w0 = ofs | (uint32_t)(lg - 2) << 13 | cm << 15 | (uint32_t)mode << 17 |
+                                ((f0 & P265R_TB_PCM) ? J_PCM : 0u) | filt << 24 | raw(fh0) << 26 | raw(fh1) << 27 |
+                                coded(fh0) << 28 | coded(fh1) << 29 | (m == full ? J_ALL : 0u) | (m == 0 ? J_NONE : 0u);
+            const uint32_t w2 = (uint32_t)m;
+            // fast path: one contiguous run of available units [ulo, uhi] -> sample bounds [fa, la]
 #ifndef P265R_FAST16
 #define P265R_FAST16 1
 #endif
             const bool fast_size = (c == 0 && n <= (P265R_FAST16 ? 16 : 8)) || (cm == 3u && n <= (g.quad & 4 ? 4 : 8));
-            if (fast_size && !(f0 & P265R_TB_PCM)) {
-                const int US = c ? 1 : 2;
-                if (m == 0) {
-                    w5 = J5_FAST;
-                } else {
-                    const int ulo = __ffsll((long long)m) - 1, uhi = 63 - __clzll((long long)m);
-                    const unsigned long long run = (uhi >= 63 ? ~0ull : ((2ull << uhi) - 1ull)) & ~((1ull << ulo) - 1ull);
-                    if (m == run) {
-                        auto first = [&](int u) { return u < L ? (u << US) : (u == L ? 2 * n : 2 * n + 1 + ((u - L - 1) << US)); };
-                        auto last = [&](int u) { return u < L ? ((u + 1) << US) - 1 : (u == L ? 2 * n : 2 * n + ((u - L) << US)); };
-                        w5 = J5_FAST | (uint32_t)first(ulo) | (uint32_t)last(uhi) << 8;
-                    }
-                }
-            }
-            J.w[5] = w5;
-            J.w[6] = J.w[7] = 0;
-            const uint32_t w5s = J.w[5] | ((J.w[1] >> 21) & 1u ? kJ5Bit32 : 0u);
-            if (kl) sj[slot] = LumaJobLds{J.w[0], J.w[2], J.w[3], w5s};
-            else if (slot < kMaxCtuChroma) sc[slot] = ChromaJobLds{J.w[0], J.w[2], J.w[3], J.w[4], w5s};
+            const int US = c ? 1 : 2;
+            const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);   // mhi: bit 32 only
+            const int ulo = mlo ? __ffs((int)mlo) - 1 : 32;
+            const int uhi = mhi ? 32 : 31 - __clz((int)(mlo | 1u));
+            const unsigned long long run = ((2ull << uhi) - 1ull) & ~((1ull << ulo) - 1ull);
+            const int fa = ulo < L ? (ulo << US) : (ulo == L ? 2 * n : 2 * n + 1 + ((ulo - L - 1) << US));
+            const int la = uhi < L ? ((uhi + 1) << US) - 1 : (uhi == L ? 2 * n : 2 * n + ((uhi - L) << US));
+            const bool fast = fast_size && !(f0 & P265R_TB_PCM) && (m == 0 || m == run);
+            const uint32_t w5 = !fast ? 0u : (m == 0 ? J5_FAST : (J5_FAST | (uint32_t)fa | (uint32_t)la << 8));
+            const uint32_t w5s = w5 | (mhi ? kJ5Bit32 : 0u);
+            if (keep && kl) sj[slot] = LumaJobLds{w0, w2, off0, w5s};
+            else if (keep && slot < kMaxCtuChroma) sc[slot] = ChromaJobLds{w0, w2, off0, off1, w5s};
         }
     }
     const int n_luma = out_l, n_chroma = min(out_c, kMaxCtuChroma);
@@ -337,8 +333,13 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     }
     for (int base = 0; base < n_chroma; base += 64) {
         const int s = base + lane;
-        uint32_t qb, qc;
-        if (s < n_chroma) chead[s] = ((g.quad & 2) && s + 3 < n_chroma && cquad_jobs(sc + s, P.zero_off, qb, qc)) ? 1 : 0;
+        uint32_t qb = 0, qc = 0;
+        if (s < n_chroma) {
+            const bool q = (g.quad & 2) && s + 3 < n_chroma && cquad_jobs(sc + s, P.zero_off, qb, qc);
+            chead[s] = q ? 1 : 0;
+            cq_base[s] = qb;
+            cq_codes[s] = qc;
+        }
     }
     __syncthreads();
     int c_out = 0;
@@ -349,12 +350,11 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const bool emit = valid && !absorbed;
         const unsigned long long me_ = __ballot(emit);
         const ChromaJobLds c = valid ? sc[s] : ChromaJobLds{0, 0, 0, 0, 0};
-        const uint32_t w1 = job_w1(angtab, c.w0, c.w5);
+        const uint32_t w1 = job_w1(c.w0, c.w5);
         if (emit) {
             IntraJob J;
-            uint32_t qb = 0, qc = 0;
-            if (chead[s] && cquad_jobs(sc + s, P.zero_off, qb, qc)) {
-                J = make_cquad(sc + s, qb, qc, P.zero_off);
+            if (chead[s]) {
+                J = make_cquad(sc + s, cq_base[s], cq_codes[s], P.zero_off);
             } else {
                 J.w[0] = c.w0; J.w[1] = w1; J.w[2] = c.w2; J.w[3] = c.w3;
                 J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const bool emit = valid && !absorbed;
         const unsigned long long me_ = __ballot(emit);
         const LumaJobLds l = valid ? sj[s] : LumaJobLds{0, 0, 0, 0};
-        const uint32_t w1 = job_w1(angtab, l.w0, l.w5);
+        const uint32_t w1 = job_w1(l.w0, l.w5);
         if (emit) {
             const IntraJob J = head[s] ? make_quad(sj + s) : luma_job(l, P.zero_off, w1);
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + n_out + rank(me_));

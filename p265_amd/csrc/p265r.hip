@@ -406,8 +406,11 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
         int8_t ang[35];
         int16_t inv[35];
         for (int i = 0; i < 35; ++i) { ang[i] = (int8_t)kIntraPredAngle[i]; inv[i] = (int16_t)kInvAngle[i]; }
+        uint32_t angw[35];
+        for (int i = 0; i < 35; ++i) angw[i] = (uint32_t)(uint8_t)ang[i] | (uint32_t)(inv[i] ? -inv[i] : 256) << 8;
         e = hipMemcpyToSymbol(HIP_SYMBOL(c_angle), ang, sizeof(ang));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_inv_angle), inv, sizeof(inv));
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_angw), angw, sizeof(angw));
     }
     if (e != hipSuccess) {
         int rc = hip_fail(e, "p265r_create");
@@ -435,6 +438,7 @@ void p265r_destroy(p265r_ctx* ctx) {
 int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p265r_batch** out) {
     if (!ctx || !pics || n_pics <= 0 || !out) return P265R_EINVAL;
     *out = nullptr;
+    if (n_pics > 65535) return P265R_ERANGE;                     // pictures index a grid dimension
     for (int i = 0; i < n_pics; ++i) {
         int rc = validate_picture(ctx, pics[i]);
         if (rc) return rc;
@@ -733,7 +737,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (recon && ctx->schedule == 1 && !(skip & 2)) {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
         // of the residuals, timed with the residual phase
-        intra_prep_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g, b->view);
+        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, 0, s>>>(b->d_pics, g, b->view);
         ++tm.residual_launches;
     }
     if (b->dbk) {
