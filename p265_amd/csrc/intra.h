@@ -144,13 +144,14 @@ __host__ __device__ __forceinline__ unsigned long long ref_avail_mask(int c, int
     const int half = L >> 1;
     const int zc = morton4(xc >> 2, yc >> 2);
     const bool fl = (flags & 1u) != 0, ft = (flags & 2u) != 0, ftl = (flags & 4u) != 0, ftr = (flags & 8u) != 0;
-    const bool left = xc > 0 || fl;
+    // (bitwise & / |: a short-circuit && / || becomes a divergent branch)
+    const bool left = (xc > 0) | fl;
     const int zbl = morton4(max(xc - 1, 0) >> 2, min(yc + nl, ctb - 1) >> 2);
-    const bool bl = yc + nl < ctb && (xc == 0 ? fl : zbl < zc);
-    const bool corner = xc > 0 ? (yc > 0 || ft) : (yc > 0 ? fl : ftl);
-    const bool top = yc > 0 || ft;
+    const bool bl = (yc + nl < ctb) & (xc == 0 ? fl : zbl < zc);
+    const bool corner = xc > 0 ? ((yc > 0) | ft) : (yc > 0 ? fl : ftl);
+    const bool top = (yc > 0) | ft;
     const int ztr = morton4(min(xc + nl, ctb - 1) >> 2, max(yc - 1, 0) >> 2);
-    const bool tr = xc + nl < ctb ? (yc > 0 ? ztr < zc : ft) : (yc == 0 && ftr);
+    const bool tr = xc + nl < ctb ? (yc > 0 ? ztr < zc : ft) : ((yc == 0) & ftr);
     // bits [lo, hi) for 0 <= lo, hi <= 33 (empty when hi <= lo)
     auto bits = [](int lo, int hi) -> unsigned long long { return ((1ull << hi) - 1ull) & ~((1ull << lo) - 1ull); };
     const int u_min = max(0, (y0 + yc + 2 * nl - h) >> 2);        // units below the picture: u < u_min

@@ -246,26 +246,34 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const int t = base + lane;
         const bool valid = t < cnt;
         const uint4 cv = rv[ci];
-        // words 0, 1 (position, size, component, mode, flags) of t - 1; words 0, 1, 3 of t + 1
-        uint4 pv = make_uint4(from_prev_lane(cv.x), from_prev_lane(cv.y), 0u, 0u);
-        uint4 nv = make_uint4(from_next_lane(cv.x), from_next_lane(cv.y), 0u, from_next_lane(cv.w));
-        if (ci > 0 && lane == 0) {
-            pv.x = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci - 1].x, 63);
-            pv.y = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci - 1].y, 63);
-        }
-        if (ci == 0 && lane == 0) pv = make_uint4(0u, 0u, 0u, 0u);
-        if (ci + 1 < kPrepChunks && lane == 63) {
-            nv.x = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci + 1].x, 0);
-            nv.y = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci + 1].y, 0);
-            nv.w = (uint32_t)__builtin_amdgcn_readlane((int)rv[ci + 1].w, 0);
-        }
-        if (ci + 1 == kPrepChunks && lane == 63) nv = make_uint4(0u, 0u, 0u, 0u);
-        p265r_tb rec{}, prev{}, next{};
-        if (valid) rec = as_tb(cv);
-        if (valid && t > 0) prev = as_tb(pv);
-        if (valid && t + 1 < cnt) next = as_tb(nv);
-        const bool cr_taken = valid && t > 0 && tb_same_tu_chroma(prev, rec);
-        const bool keep = valid && !cr_taken;
+        // words 0, 1 (position, size, component, mode, flags) of t - 1; words 0, 1, 3 of t + 1 --
+        // neighbouring lanes (DPP), across the chunk edges by v_readlane, selected without branches
+        const uint32_t pe_x = ci > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)rv[ci > 0 ? ci - 1 : 0].x, 63) : 0u;
+        const uint32_t pe_y = ci > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)rv[ci > 0 ? ci - 1 : 0].y, 63) : 0u;
+        const int cn = ci + 1 < kPrepChunks ? ci + 1 : ci;
+        const uint32_t ne_x = ci + 1 < kPrepChunks ? (uint32_t)__builtin_amdgcn_readlane((int)rv[cn].x, 0) : 0u;
+        const uint32_t ne_y = ci + 1 < kPrepChunks ? (uint32_t)__builtin_amdgcn_readlane((int)rv[cn].y, 0) : 0u;
+        const uint32_t ne_w = ci + 1 < kPrepChunks ? (uint32_t)__builtin_amdgcn_readlane((int)rv[cn].w, 0) : 0u;
+        const bool has_prev = valid & (t > 0), has_next = valid & (t + 1 < cnt);
+        // the DPP moves are pinned here (empty asm): left to the compiler they sink into divergent
+        // branches of their selects, each with its own exec-mask save / restore
+        uint32_t dp0 = from_prev_lane(cv.x), dp1 = from_prev_lane(cv.y);
+        uint32_t dn0 = from_next_lane(cv.x), dn1 = from_next_lane(cv.y), dn3 = from_next_lane(cv.w);
+        asm volatile("" : "+v"(dp0), "+v"(dp1), "+v"(dn0), "+v"(dn1), "+v"(dn3));
+        const uint32_t p0 = has_prev ? (lane == 0 ? pe_x : dp0) : 0u;
+        const uint32_t p1 = has_prev ? (lane == 0 ? pe_y : dp1) : 0u;
+        const uint4 nv = make_uint4(lane == 63 ? ne_x : dn0, lane == 63 ? ne_y : dn1, 0u, lane == 63 ? ne_w : dn3);
+        p265r_tb rec = as_tb(valid ? cv : make_uint4(0u, 0u, 0u, 0u));
+        p265r_tb next = as_tb(has_next ? nv : make_uint4(0u, 0u, 0u, 0u));
+        // tb_same_tu_chroma on the raw words: word 0 = x | y << 16, word 1 = log2 | c_idx << 8 |
+        // pred_mode << 16 | flags << 24 (Cb then Cr of one TU: same position, size, mode, PCM flag)
+        auto same_tu = [](uint32_t cb0, uint32_t cb1, uint32_t cr0, uint32_t cr1) {   // (bitwise: no short circuit)
+            return (cb0 == cr0) & ((cb1 & 0xff00u) == 0x0100u) & ((cr1 & 0xff00u) == 0x0200u) &
+                   (((cb1 ^ cr1) & (0x00ff00ffu | (uint32_t)P265R_TB_PCM << 24)) == 0u);
+        };
+        const bool cr_taken = has_prev & same_tu(p0, p1, cv.x, cv.y);
+        const bool keep = valid & !cr_taken;
+        const bool pair_next = has_next & same_tu(cv.x, cv.y, nv.x, nv.y);
         const bool kl = keep && rec.c_idx == 0;
         const unsigned long long ml = __ballot(kl), mc = __ballot(keep && !kl);
         const int slot = kl ? out_l + rank(ml) : out_c + rank(mc);
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         {
             const int lg = max((int)rec.log2_size, 2), n = 1 << lg, c = rec.c_idx;
             const int sub = c ? 1 : 0;
-            const bool pair = c == 1 && t + 1 < cnt && tb_same_tu_chroma(rec, next);
+            const bool pair = pair_next;
             const int xr = (int)rec.x - (x0 >> sub), yr = (int)rec.y - (y0 >> sub);
             const uint32_t ofs = c == 0 ? (uint32_t)(yr * 64 + xr) : (uint32_t)(4096 + yr * 32 + xr);
             const uint32_t cm = c == 0 ? 0u : (pair ? 3u : (uint32_t)c);
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const unsigned long long full = (1ull << (2 * L + 1)) - 1ull;
             // ---- filtering decision (8.4.4.2.3), luma only in 4:2:0 ---------------------------
             const int dist = min(abs(mode - 26), abs(mode - 10));
-            const bool fon = c == 0 && n != 4 && mode != 1 && dist > (n == 8 ? 7 : (n == 16 ? 1 : 0));
+            const bool fon = (c == 0) & (n != 4) & (mode != 1) & (dist > (n == 8 ? 7 : (n == 16 ? 1 : 0)));
             const uint32_t filt = fon ? ((n == 32 && g.strong) ? 2u : 1u) : 0u;
             const uint32_t f0 = rec.flags;
             const uint32_t f1 = pair ? next.flags : 0u;
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
 #ifndef P265R_FAST16
 #define P265R_FAST16 1
 #endif
-            const bool fast_size = (c == 0 && n <= (P265R_FAST16 ? 16 : 8)) || (cm == 3u && n <= (g.quad & 4 ? 4 : 8));
+            const bool fast_size = ((c == 0) & (n <= (P265R_FAST16 ? 16 : 8))) | ((cm == 3u) & (n <= (g.quad & 4 ? 4 : 8)));
             const int US = c ? 1 : 2;
             const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);   // mhi: bit 32 only
             const int ulo = mlo ? __ffs((int)mlo) - 1 : 32;
@@ -317,7 +325,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const unsigned long long run = ((2ull << uhi) - 1ull) & ~((1ull << ulo) - 1ull);
             const int fa = ulo < L ? (ulo << US) : (ulo == L ? 2 * n : 2 * n + 1 + ((ulo - L - 1) << US));
             const int la = uhi < L ? ((uhi + 1) << US) - 1 : (uhi == L ? 2 * n : 2 * n + ((uhi - L) << US));
-            const bool fast = fast_size && !(f0 & P265R_TB_PCM) && (m == 0 || m == run);
+            const bool fast = fast_size & !(f0 & P265R_TB_PCM) & ((m == 0) | (m == run));
             const uint32_t w5 = !fast ? 0u : (m == 0 ? J5_FAST : (J5_FAST | (uint32_t)fa | (uint32_t)la << 8));
             const uint32_t w5s = w5 | (mhi ? kJ5Bit32 : 0u);
             if (keep && kl) sj[slot] = LumaJobLds{w0, w2, off0, w5s};
