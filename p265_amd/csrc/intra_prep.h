@@ -70,16 +70,17 @@ constexpr uint32_t kJ5Bit32 = 1u << 16;
 struct LumaJobLds { uint32_t w0, w2, w3, w5; };
 
 // the four jobs at slots s..s+3 are the fast 4x4 luma TBs of one 8x8 region, in z-order
+// (straight-line: every lane of the prep wave evaluates it; bitwise & instead of early returns)
 __device__ __forceinline__ bool quad_jobs(const LumaJobLds* j) {
     const uint32_t o = j[0].w0 & 0x1fffu;
-    if ((o & 7u) || ((o >> 6) & 7u)) return false;                 // region origin on the 8x8 grid
+    bool ok = ((o & 7u) | ((o >> 6) & 7u)) == 0u;                  // region origin on the 8x8 grid
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t w0 = j[i].w0;
-        if (!(j[i].w5 & J5_FAST) || ((w0 >> 13) & 15u)) return false;     // fast, 4x4, luma
-        if ((w0 & 0x1fffu) != o + (uint32_t)((i & 1) * 4 + (i >> 1) * 256)) return false;
+        ok &= ((j[i].w5 & J5_FAST) != 0u) & (((w0 >> 13) & 15u) == 0u) &    // fast, 4x4, luma
+              ((w0 & 0x1fffu) == o + (uint32_t)((i & 1) * 4 + (i >> 1) * 256));
     }
-    return true;
+    return ok;
 }
 
 __device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j) {
@@ -108,36 +109,32 @@ struct ChromaJobLds { uint32_t w0, w2, w3, w4, w5; };
 // the four jobs at slots s..s+3 are fast Cb+Cr 4x4 pairs of one 8x8 chroma region, in z-order,
 // and their eight residuals are addressable as base + 16 * code (code <= 14; 15 = zero block):
 // coded chroma 4x4 TBs of one class are packed in decode order at upload (p265r.hip), so the
-// coded TBs of a region normally sit in consecutive 16-sample slots
+// coded TBs of a region normally sit in consecutive 16-sample slots.  Straight-line, as quad_jobs.
 __device__ __forceinline__ bool cquad_jobs(const ChromaJobLds* j, uint32_t zero_off, uint32_t& base, uint32_t& codes) {
     const uint32_t o = j[0].w0 & 0x1fffu;
-    if (o < 4096u || ((o - 4096u) & 7u) || (((o - 4096u) >> 5) & 7u)) return false;   // 8x8 chroma grid
+    bool ok = (o >= 4096u) & ((((o - 4096u) & 7u) | (((o - 4096u) >> 5) & 7u)) == 0u);   // 8x8 chroma grid
+    uint32_t off[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t w0 = j[i].w0;
-        if (!(j[i].w5 & J5_FAST) || ((w0 >> 13) & 3u) || ((w0 >> 15) & 3u) != 3u) return false;   // fast 4x4 pair
-        if ((w0 & 0x1fffu) != o + (uint32_t)((i & 1) * 4 + (i >> 1) * 128)) return false;
+        ok &= ((j[i].w5 & J5_FAST) != 0u) & (((w0 >> 13) & 3u) == 0u) & (((w0 >> 15) & 3u) == 3u) &   // fast 4x4 pair
+              ((w0 & 0x1fffu) == o + (uint32_t)((i & 1) * 4 + (i >> 1) * 128));
+        off[2 * i] = j[i].w3;
+        off[2 * i + 1] = j[i].w4;
     }
     int32_t mn = INT32_MAX;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t off = (i & 1) ? j[i >> 1].w4 : j[i >> 1].w3;
-        if (off != zero_off) mn = min(mn, (int32_t)off);
-    }
+    for (int i = 0; i < 8; ++i) mn = off[i] != zero_off ? min(mn, (int32_t)off[i]) : mn;
     base = mn == INT32_MAX ? zero_off : (uint32_t)mn;
     codes = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint32_t off = (i & 1) ? j[i >> 1].w4 : j[i >> 1].w3;
-        uint32_t code = 15u;
-        if (off != zero_off) {
-            const int64_t d = (int64_t)(int32_t)off - mn;
-            if ((d & 15) || d > 14 * 16) return false;
-            code = (uint32_t)(d >> 4);
-        }
-        codes |= code << (4 * i);                 // i = 2q + h -> bit 8q + 4h
+        const uint32_t d = off[i] - (uint32_t)mn;                 // >= 0 for the coded ones: mn is their minimum
+        const bool z = off[i] == zero_off;
+        ok &= z | (((d & 15u) == 0u) & (d <= 14u * 16u));
+        codes |= (z ? 15u : (d >> 4) & 15u) << (4 * i);            // i = 2q + h -> bit 8q + 4h
     }
-    return true;
+    return ok;
 }
 
 __device__ __forceinline__ IntraJob make_cquad(const ChromaJobLds* j, uint32_t base, uint32_t codes, uint32_t zero_off) {
@@ -350,23 +347,34 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         }
     }
     __syncthreads();
+    // ---- emission: a slot is absorbed when one of the three before it heads a quad; the heads of
+    // a 64-slot window come from one ballot (+ the previous window's last three), the LDS reads are
+    // unconditional (clamped), only the stores are predicated
+    auto absorbed_mask = [](unsigned long long H, unsigned long long Hp) {
+        return (H << 1) | (H << 2) | (H << 3) | (Hp >> 63) | (Hp >> 62) | (Hp >> 61);
+    };
     int c_out = 0;
+    unsigned long long hp = 0;
     for (int base = 0; base < n_chroma; base += 64) {
         const int s = base + lane;
         const bool valid = s < n_chroma;
-        const bool absorbed = valid && ((s >= 1 && chead[s - 1]) || (s >= 2 && chead[s - 2]) || (s >= 3 && chead[s - 3]));
-        const bool emit = valid && !absorbed;
+        const int s1 = min(s, n_chroma - 1);                          // in-bounds LDS reads for every lane
+        const int sq = min(s, kMaxCtuChroma - 4);                     // (a head's quad: sq = s)
+        const bool hd = valid & (chead[s1] != 0);
+        const unsigned long long H = __ballot(hd);
+        const bool emit = valid & !((absorbed_mask(H, hp) >> lane) & 1ull);
+        hp = H;
         const unsigned long long me_ = __ballot(emit);
-        const ChromaJobLds c = valid ? sc[s] : ChromaJobLds{0, 0, 0, 0, 0};
+        const ChromaJobLds c = sc[s1];
         const uint32_t w1 = job_w1(c.w0, c.w5);
+        IntraJob J;
+        if (hd) {
+            J = make_cquad(sc + sq, cq_base[sq], cq_codes[sq], P.zero_off);
+        } else {
+            J.w[0] = c.w0; J.w[1] = w1; J.w[2] = c.w2; J.w[3] = c.w3;
+            J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
+        }
         if (emit) {
-            IntraJob J;
-            if (chead[s]) {
-                J = make_cquad(sc + s, cq_base[s], cq_codes[s], P.zero_off);
-            } else {
-                J.w[0] = c.w0; J.w[1] = w1; J.w[2] = c.w2; J.w[3] = c.w3;
-                J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
-            }
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + rank(me_));
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
@@ -374,16 +382,20 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         c_out += __popcll(me_);
     }
     int n_out = 0;
+    hp = 0;
     for (int base = 0; base < n_luma; base += 64) {
         const int s = base + lane;
         const bool valid = s < n_luma;
-        const bool absorbed = valid && ((s >= 1 && head[s - 1]) || (s >= 2 && head[s - 2]) || (s >= 3 && head[s - 3]));
-        const bool emit = valid && !absorbed;
+        const int s1 = min(s, n_luma - 1), sq = min(s, kMaxCtuLuma - 4);
+        const bool hd = valid & (head[s1] != 0);
+        const unsigned long long H = __ballot(hd);
+        const bool emit = valid & !((absorbed_mask(H, hp) >> lane) & 1ull);
+        hp = H;
         const unsigned long long me_ = __ballot(emit);
-        const LumaJobLds l = valid ? sj[s] : LumaJobLds{0, 0, 0, 0};
+        const LumaJobLds l = sj[s1];
         const uint32_t w1 = job_w1(l.w0, l.w5);
+        const IntraJob J = hd ? make_quad(sj + sq) : luma_job(l, P.zero_off, w1);
         if (emit) {
-            const IntraJob J = head[s] ? make_quad(sj + s) : luma_job(l, P.zero_off, w1);
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + n_out + rank(me_));
             dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
             dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
