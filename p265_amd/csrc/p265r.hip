@@ -113,6 +113,12 @@ struct p265r_ctx {
     int pipeline = 1;
     int next_lane = 0;
     std::vector<hipStream_t> lanes;   // lanes[0] == stream
+    // job prep forked onto a second stream per lane (P265R_FORK_PREP, default on): the prep
+    // kernel (latency-bound, LDS/VGPR-limited occupancy) runs beside the residual kernels
+    // (HBM-bound) instead of after them; the intra kernel waits for both
+    int fork_prep = 1;
+    std::vector<hipStream_t> aux;     // aux[i]: lane i's prep stream (created on first use)
+    std::vector<hipEvent_t> fork_ev, join_ev;
     std::string describe;             // p265r_describe text
 };
 
@@ -386,7 +392,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     // experiment / test knobs read from the environment (bench.py refuses to run with any set)
     for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_DEBUG_SYNC", "P265R_SAO_ROWS", "P265R_SKIP",
-                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES"})
+                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES", "P265R_FORK_PREP"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
@@ -394,6 +400,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::atoi(v) != 0;
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 16) ctx->row_waves = w;
@@ -425,7 +432,11 @@ void p265r_destroy(p265r_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     for (hipStream_t st : ctx->lanes) (void)hipStreamSynchronize(st);
+    for (hipStream_t st : ctx->aux) if (st) (void)hipStreamSynchronize(st);
     if (ctx->pending) p265r_batch_free(ctx, ctx->pending);
+    for (hipStream_t st : ctx->aux) if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t e : ctx->fork_ev) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->join_ev) if (e) (void)hipEventDestroy(e);
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
     for (auto& e : ctx->spare) (void)hipEventDestroy(e);
     for (size_t i = 1; i < ctx->lanes.size(); ++i) (void)hipStreamDestroy(ctx->lanes[i]);
@@ -710,6 +721,30 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // run are still in place, so the output is unchanged while the skipped phase costs nothing
     const int skip = b->runs > 0 ? ctx->skip : 0;
     ++b->runs;
+    const bool prep = recon && ctx->schedule == 1 && !(skip & 2);
+    hipStream_t ps = s;                              // the prep kernel's stream
+    if (prep && ctx->fork_prep) {
+        const size_t li = (size_t)b->lane;
+        if (ctx->aux.size() <= li) {
+            ctx->aux.resize(li + 1, nullptr); ctx->fork_ev.resize(li + 1, nullptr); ctx->join_ev.resize(li + 1, nullptr);
+        }
+        if (!ctx->aux[li]) {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->aux[li], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->fork_ev[li], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->join_ev[li], hipEventDisableTiming));
+        }
+        ps = ctx->aux[li];
+        HIP_TRY(hipEventRecord(ctx->fork_ev[li], s));
+        HIP_TRY(hipStreamWaitEvent(ps, ctx->fork_ev[li], 0));
+    }
+    if (prep) {
+        // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
+        // of the residuals, timed with the residual phase; enqueued first so that, forked, its
+        // waves start before the residual kernels fill the chip
+        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, 0, ps>>>(b->d_pics, g, b->view);
+        ++tm.residual_launches;
+        if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[(size_t)b->lane], ps));
+    }
     if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
         residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl);
         ++tm.residual_launches;
@@ -734,12 +769,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (recon && ctx->schedule == 1 && !(skip & 2)) {
-        // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
-        // of the residuals, timed with the residual phase
-        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, 0, s>>>(b->d_pics, g, b->view);
-        ++tm.residual_launches;
-    }
+    if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[(size_t)b->lane], 0));
     if (b->dbk) {
         // deblocking edge / QpY map: depends on the records only
         dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
@@ -779,9 +809,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
-    if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && !(skip & 4)) {
+    if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && g.h % 8 == 0 && !(skip & 4)) {
         // SAO only, CTB 32 / 64: the 16-samples-per-lane strip kernel (sao_strip16.h), one wave per
-        // (picture, CTB row, component, 992-sample strip), 4 waves per block, blocks dealt XCD-aware
+        // (picture, CTB row, component, 992-sample strip), 4 waves per block, blocks dealt XCD-aware;
+        // it filters 4-row chunks and takes plane heights in multiples of 4 (luma a multiple of
+        // MinCbSizeY >= 8 in a conforming stream; anything else goes to the 4-B strip kernel)
         const long long waves = (long long)sao16_units(g) * b->n_pics;
         if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
         const unsigned blocks = (unsigned)((waves + 3) / 4 + 7) / 8 * 8;
@@ -898,6 +930,7 @@ int p265r_sync(p265r_ctx* ctx) {
     if (!ctx) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     for (hipStream_t st : ctx->lanes) HIP_TRY(hipStreamSynchronize(st));
+    for (hipStream_t st : ctx->aux) if (st) HIP_TRY(hipStreamSynchronize(st));
     return P265R_OK;
 }
 
@@ -921,11 +954,11 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
     const int n = snprintf(tmp, sizeof(tmp),
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
-        "\"pipeline\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
+        "\"pipeline\": %d, \"fork_prep\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, W=8 register-lean while other lanes have work",
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
-        ctx->pipeline, ctx->num_cus,
+        ctx->pipeline, ctx->fork_prep, ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG
         1,
 #else

@@ -153,6 +153,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     //   class 0: a = (cur j, cur j-1, 3)  b = (cur j+1, cur j, 1);  class 1: a = up j, b = dn j (shift 0)
     //   class 2: a = (up j, up j-1, 3)    b = (dn j+1, dn j, 1);    class 3: a = (up j+1, up j, 1)  b = (dn j, dn j-1, 3)
     const uint32_t sha = ecls == 1 ? 0u : (c3 ? 1u : 3u), shb = ecls == 1 ? 0u : (c3 ? 3u : 1u);
+    // the same as sources of one shifted row view: a = alignbyte(V[j + ea], V[j + ea - 1], sha) of
+    // V = the a-row (class 0: this row, else the row above), b likewise with eb, the b-row
+    const bool ea = ecls == 1 || c3, eb = !c3;
 
     // ---- byte masks: which of the lane's 16 samples may change, per row kind --------------------
     // neighbour (dx, dy) of sample i of row y is usable iff inside the picture and its CTB allowed;
@@ -226,17 +229,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
 #pragma unroll
                     for (int j = 0; j < 4; ++j) nfm[j] = nf[ny + min(((Xc + 4 * j) << sub) >> 3, g.nf_w - 1)] ? 0xffffffffu : 0u;
                 }
-                const uint32_t* m = y == yb ? m_top : (y == ylast ? m_bot : m_mid);
+                // plane heights are multiples of 4 samples (host-checked), so a chunk's first row is
+                // the only one that can be the CTB row's first, its last the only one that can be the last
+                const uint32_t* m = r == 0 ? (y == yb ? m_top : m_mid) : (r == K - 1 ? (y == ylast ? m_bot : m_mid) : m_mid);
+                // neighbours per lane class: a from row U (this row for class 0, the row above
+                // otherwise), b from row D (this row / the row below), each horizontally shifted
+                // by the class's dx: one select per dword of U / D and of their shifted views,
+                // shared by the row's four dwords
+                uint32_t U[6], D[6], Ua[5], Db[5];
+#pragma unroll
+                for (int j = -1; j <= 4; ++j) {
+                    U[j + 1] = c0 ? dw(k, j) : dw(k - 1, j);
+                    D[j + 1] = c0 ? dw(k, j) : dw(k + 1, j);
+                }
+#pragma unroll
+                for (int j = -1; j <= 3; ++j) {
+                    Ua[j + 1] = ea ? U[j + 2] : U[j + 1];
+                    Db[j + 1] = eb ? D[j + 2] : D[j + 1];
+                }
                 uint32_t out[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t cur = dw(k, j);
-                    const uint32_t a_hi = c0 ? cur : (c3 ? dw(k - 1, j + 1) : dw(k - 1, j));
-                    const uint32_t a_lo = c0 ? dw(k, j - 1) : (c2 ? dw(k - 1, j - 1) : dw(k - 1, j));
-                    const uint32_t b_hi = c0 ? dw(k, j + 1) : (c2 ? dw(k + 1, j + 1) : dw(k + 1, j));
-                    const uint32_t b_lo = c0 ? cur : (c3 ? dw(k + 1, j - 1) : dw(k + 1, j));
-                    const uint32_t a = __builtin_amdgcn_alignbyte(a_hi, a_lo, sha);
-                    const uint32_t b = __builtin_amdgcn_alignbyte(b_hi, b_lo, shb);
+                    const uint32_t a = __builtin_amdgcn_alignbyte(Ua[j + 1], Ua[j], sha);
+                    const uint32_t b = __builtin_amdgcn_alignbyte(Db[j + 1], Db[j], shb);
                     const uint32_t v_lo = split_lo(cur), v_hi = split_hi(cur);
                     uint32_t sel_lo = edge16(v_lo, split_lo(a), split_lo(b));
                     uint32_t sel_hi = edge16(v_hi, split_hi(a), split_hi(b));

@@ -43,10 +43,11 @@ def _check(recon_mod, params, pics, label=""):
 
 # row pipeline variants: waves per workgroup; P265R_QUAD job merging (bit 0 luma 4x4 quads, bit 1
 # chroma 4x4 quads, bit 2 Cb+Cr 8x8 pairs on the general path instead of the fast one); the
-# register-lean W = 8 build (P265R_LEAN=1) and fair CU sharing off (P265R_FAIR=0); the row queue with
+# register-lean W = 8 build (P265R_LEAN=1), fair CU sharing off (P265R_FAIR=0) and job prep on the
+# batch stream (P265R_FORK_PREP=0); the row queue with
 # the luma chain not leading (P265R_LUMA_LEAD=0) and leading by more rows than a picture has (40)
 ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
-                "rows_lean": {"P265R_ROW_WAVES": "8", "P265R_LEAN": "1", "P265R_FAIR": "0"},
+                "rows_lean": {"P265R_ROW_WAVES": "8", "P265R_LEAN": "1", "P265R_FAIR": "0", "P265R_FORK_PREP": "0"},
                 "rows10": {"P265R_ROW_WAVES": "10", "P265R_LUMA_LEAD": "0"}, "rows12": {"P265R_ROW_WAVES": "12"},
                 "rows16": {"P265R_ROW_WAVES": "16", "P265R_LUMA_LEAD": "40"},
                 "rows4": {"P265R_ROW_WAVES": "4", "P265R_QUAD": "1"},

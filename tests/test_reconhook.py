@@ -91,8 +91,9 @@ def _build(rng, hook_side):
     for k, (x, y, lg) in enumerate(rest):
         yb, cbb = _blk(rng, 1 << lg), _blk(rng, 1 << (lg - 1))
         cus.append(_cu(x, y, lg, 0, {(x, y): (7 * k + 1) % 35}, 4, [_leaf(x, y, lg, 0, [1, k % 2, 0], [yb, cbb, None])]))
-    sao = NS(sao_type_idx=[2, 1, 0], sao_offset_abs=[[1, 2, 3, 4]] * 3, sao_offset_sign=[[1, 0, 1, 0]] * 3,
-             sao_band_position=[0, 7, 0], sao_eo_class=[1, 0, 0])
+    # Cr shares Cb's SaoTypeIdx (7.4.9.3.2), with its own band position
+    sao = NS(sao_type_idx=[2, 1, 1], sao_offset_abs=[[1, 2, 3, 4]] * 3, sao_offset_sign=[[1, 0, 1, 0]] * 3,
+             sao_band_position=[0, 7, 3], sao_eo_class=[1, 0, 0])
     ctu = NS(addr_rs=0, slice_addr=0, sao=sao)
     sh = NS(slice_sao_luma_flag=1, slice_sao_chroma_flag=1)
     pps = NS(pps_deblocking_filter_disabled_flag=0, pps_loop_filter_across_slices_enabled_flag=1,
@@ -114,7 +115,7 @@ def _build(rng, hook_side):
         b.add_cu(x, y, lg, 0, [(7 * k + 1) % 35, 0, 0, 0], 4, 30, 29, 28,
                  [dict(x=x, y=y, log2=lg, blk=0, cbf=[1, k % 2, 0], tskip=[0, 0, 0],
                        coef=[leaf.trans_coeff_level[0].T, leaf.trans_coeff_level[1].T, None])])
-    b.add_ctu(0, sao_type=(2, 1, 0), sao_abs=[[1, 2, 3, 4]] * 3, sao_sign=[[1, 0, 1, 0]] * 3, sao_band=(0, 7, 0),
+    b.add_ctu(0, sao_type=(2, 1, 1), sao_abs=[[1, 2, 3, 4]] * 3, sao_sign=[[1, 0, 1, 0]] * 3, sao_band=(0, 7, 3),
               sao_eo=(1, 0, 0), deblocking=True, beta_offset_div2=2, tc_offset_div2=-1)
     return params, b.finish()
 
