@@ -184,9 +184,6 @@ __device__ __forceinline__ uint32_t job_w1(uint32_t w0, uint32_t w5) {
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g, BatchView v) {
     __shared__ LumaJobLds sj[kMaxCtuLuma];
     __shared__ ChromaJobLds sc[kMaxCtuChroma];
-    __shared__ uint8_t head[kMaxCtuLuma];
-    __shared__ uint8_t chead[kMaxCtuChroma];
-    __shared__ uint32_t cq_base[kMaxCtuChroma], cq_codes[kMaxCtuChroma];   // chroma quads found at detection
     const DevPic P = pics[blockIdx.z];
     // CTU records from the batch layout (no wait for the DevPic load: both in flight together)
     const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.z * g.wc * g.hc;
@@ -331,25 +328,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     }
     const int n_luma = out_l, n_chroma = min(out_c, kMaxCtuChroma);
     __syncthreads();
-    // ---- 4x4 quads: slot s heads one when s..s+3 are its four fast TBs / Cb+Cr pairs ---------
-    for (int base = 0; base < n_luma; base += 64) {
-        const int s = base + lane;
-        if (s < n_luma) head[s] = ((g.quad & 1) && s + 3 < n_luma && quad_jobs(sj + s)) ? 1 : 0;
-    }
-    for (int base = 0; base < n_chroma; base += 64) {
-        const int s = base + lane;
-        uint32_t qb = 0, qc = 0;
-        if (s < n_chroma) {
-            const bool q = (g.quad & 2) && s + 3 < n_chroma && cquad_jobs(sc + s, P.zero_off, qb, qc);
-            chead[s] = q ? 1 : 0;
-            cq_base[s] = qb;
-            cq_codes[s] = qc;
-        }
-    }
-    __syncthreads();
-    // ---- emission: a slot is absorbed when one of the three before it heads a quad; the heads of
-    // a 64-slot window come from one ballot (+ the previous window's last three), the LDS reads are
-    // unconditional (clamped), only the stores are predicated
+    // ---- 4x4 quads + emission, one pass per 64-slot window: slot s heads a quad when s..s+3 are
+    // its four fast TBs / Cb+Cr pairs; a slot is absorbed when one of the three before it heads
+    // one (this window's heads from one ballot, the previous window's last three carried).  Every
+    // lane reads in-bounds LDS (clamped), only the stores are predicated; no head arrays in LDS
     auto absorbed_mask = [](unsigned long long H, unsigned long long Hp) {
         return (H << 1) | (H << 2) | (H << 3) | (Hp >> 63) | (Hp >> 62) | (Hp >> 61);
     };
@@ -358,9 +340,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     for (int base = 0; base < n_chroma; base += 64) {
         const int s = base + lane;
         const bool valid = s < n_chroma;
-        const int s1 = min(s, n_chroma - 1);                          // in-bounds LDS reads for every lane
-        const int sq = min(s, kMaxCtuChroma - 4);                     // (a head's quad: sq = s)
-        const bool hd = valid & (chead[s1] != 0);
+        const int s1 = min(s, n_chroma - 1);
+        const int sq = min(s, kMaxCtuChroma - 4);                     // (a head: sq = s)
+        uint32_t qb = 0, qc = 0;
+        const bool hd = ((g.quad & 2) != 0) & (s + 3 < n_chroma) & cquad_jobs(sc + sq, P.zero_off, qb, qc);
         const unsigned long long H = __ballot(hd);
         const bool emit = valid & !((absorbed_mask(H, hp) >> lane) & 1ull);
         hp = H;
@@ -369,7 +352,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const uint32_t w1 = job_w1(c.w0, c.w5);
         IntraJob J;
         if (hd) {
-            J = make_cquad(sc + sq, cq_base[sq], cq_codes[sq], P.zero_off);
+            J = make_cquad(sc + sq, qb, qc, P.zero_off);
         } else {
             J.w[0] = c.w0; J.w[1] = w1; J.w[2] = c.w2; J.w[3] = c.w3;
             J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
@@ -387,7 +370,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const int s = base + lane;
         const bool valid = s < n_luma;
         const int s1 = min(s, n_luma - 1), sq = min(s, kMaxCtuLuma - 4);
-        const bool hd = valid & (head[s1] != 0);
+        const bool hd = ((g.quad & 1) != 0) & (s + 3 < n_luma) & quad_jobs(sj + sq);
         const unsigned long long H = __ballot(hd);
         const bool emit = valid & !((absorbed_mask(H, hp) >> lane) & 1ull);
         hp = H;
