@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     const uint32_t bsh = (uint32_t)((32 - cls) & 31);
     const uint32_t badd = __umul24(bsh, 0x010101u) | bsh << 24;   // (32 - band position) in every byte
     const int ecls = typ == 2 ? (cls & 3) : 0;
-    const bool c0 = ecls == 0, c2 = ecls == 2, c3 = ecls == 3;
+    const bool c0 = ecls == 0, c3 = ecls == 3;
     // a = alignbyte(a_hi, a_lo, sha), b = alignbyte(b_hi, b_lo, shb) with the sources per class:
     //   class 0: a = (cur j, cur j-1, 3)  b = (cur j+1, cur j, 1);  class 1: a = up j, b = dn j (shift 0)
     //   class 2: a = (up j, up j-1, 3)    b = (dn j+1, dn j, 1);    class 3: a = (up j+1, up j, 1)  b = (dn j, dn j-1, 3)

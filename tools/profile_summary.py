@@ -51,7 +51,11 @@ def main(src, tag):
     sq = per_kernel(os.path.join(src, "sq", "sq_counter_collection.csv"))
     iso = isolated_avg(os.path.join(src, "kt", "kt_kernel_trace.csv"))
     out = {}
-    lines = ["# rocprofv3 summary `%s` (bench.py --frames 512 --steps 3 --warmup 1 --unique 2, 1080p)" % tag, "",
+    cmd = os.path.join(src, "cmd.txt")
+    what = open(cmd).read().strip() if os.path.exists(cmd) else "python bench.py --frames 512 --steps 3 --warmup 1 --unique 2"
+    if os.path.exists(os.path.join(src, "bench.json")):
+        shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+    lines = ["# rocprofv3 summary `%s` (`%s`)" % (tag, what), "",
              "avg ms = mean over the dispatches that overlap no other dispatch (the one-batch pass of",
              "bench.py); avg all = rocprofv3 --stats over every dispatch, incl. the pipelined ones.", "",
              "| kernel | calls | avg ms (isolated, n) | avg all ms | FETCH KB | WRITE KB | corrected traffic GB (2F+W) | VALU/wave | SALU/wave | LDS/wave |",
