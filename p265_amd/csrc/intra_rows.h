@@ -912,6 +912,15 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         const int tag = (j & 0xffff) << 16;
         __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 
+        // CTU header (first TB index | job counts) loaded one CTU ahead, and the next CTU's first
+        // 64 job records loaded right after this CTU's last job: a CTU then starts with its
+        // records in registers (one dependent round trip, its first residual, instead of three)
+        auto hdr_load = [&](int a) {
+            return make_uint2(gload(reinterpret_cast<const uint2*>(ctus + a)).x, *gptr(jcount + a));
+        };
+        uint2 hdr_n = hdr_load(cy * g.wc);
+        uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
+        bool pre = false;                                  // rec0 / rec1 hold this CTU's first records
         for (int cx = 0; cx < g.wc; ++cx) {
             // ---- wait for the row above (2-CTU lag) -------------------------------------
             if (cy > 0) {
@@ -924,10 +933,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             P265R_TRACE(4 | (cx << 8) | (r << 16));
             const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
             const int addr = cy * g.wc + cx;
-            // this CTU's job list (intra_prep_kernel): first job = its first TB index
-            const uint32_t tb_begin = uniform(gload(reinterpret_cast<const uint2*>(ctus + addr))).x;
-            // job counts: luma in bits 0..15, chroma (listed first) in bits 16..31 (intra_prep.h)
-            const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(*gptr(jcount + addr));
+            // this CTU's job list (intra_prep_kernel): first job = its first TB index; job counts:
+            // luma in bits 0..15, chroma (listed first) in bits 16..31 (intra_prep.h)
+            const uint32_t tb_begin = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
+            const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
+            if (cx + 1 < g.wc) hdr_n = hdr_load(addr + 1);   // in flight during this CTU
             const int n_chroma = (int)(jc >> 16);
             const int nt = comp ? n_chroma : (int)(jc & 0xffffu);
             const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
@@ -958,7 +968,6 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             // (scalar loads were measured slower: their lgkmcnt waits serialise with the LDS
             // traffic of the job)
             struct JobS { uint32_t w0, w1, w2, w3, w4, w5; };
-            uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
             auto refill = [&](int base) {
                 if (base + lane < nt) { rec0 = ld16(&jl[base + lane].w[0]); rec1 = ld16(&jl[base + lane].w[4]); }
                 else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
@@ -1004,7 +1013,12 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 return u32x2_t{0u, 0u};
             };
             JobS cur{0, 0, 0, 0, 0, 0};
-            if (nt) { refill(0); cur = sjob(0); rn = issue(cur, 0); }
+            if (nt) {
+                if (!pre) refill(0);
+                cur = sjob(0);
+                rn = issue(cur, 0);
+            }
+            pre = false;
             for (int t = 0; t < nt; ++t) {
 #ifdef P265R_JOB_STATS
                 const long long tj0 = __builtin_amdgcn_s_memtime();
@@ -1069,6 +1083,16 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #endif
             }
 
+            if (cx + 1 < g.wc) {                           // the next CTU's first 64 job records
+                const uint32_t tb2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
+                const uint32_t jc2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
+                const int nc2 = (int)(jc2 >> 16);
+                const int nt2 = comp ? nc2 : (int)(jc2 & 0xffffu);
+                const IntraJob* jl2 = jobs + tb2 + (comp ? 0 : nc2);
+                if (lane < nt2) { rec0 = ld16(&jl2[lane].w[0]); rec1 = ld16(&jl2[lane].w[4]); }
+                else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
+                pre = true;
+            }
             P265R_TRACE(5 | (cx << 8) | (r << 16));
             // ---- publish the CTU: planes (HBM), bottom line (LDS), right column (LDS) ----------
 #pragma unroll
