@@ -96,8 +96,11 @@ struct p265r_ctx {
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
                                // while other lanes have work queued (P265R_LEAN)
-    int luma_lead = 5;         // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD;
-                               // measured, 1080p W=8: lead 0/1/2/3/5/8/17 -> 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
+    int luma_lead = -1;        // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD);
+                               // -1 = by run: 8 for a batch alone, 5 beside other lanes' batches (round 3,
+                               // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
+                               // 45.5/44.9/44.4/44.7 M CTU/s; round 1, W=8: lead 0/1/2/3/5/8/17 ->
+                               // 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every phase (P265R_DEBUG_DIAG
                                // builds also trace the row kernel's waves and print placement statistics)
@@ -299,7 +302,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
         fprintf(stderr, "[p265r] rows kernel W=%d WPE=%d fair=%d grid=%d lds=%zu fs=%d per_cu=%d\n", W, WPE, g.fair, grid, lds, fs, per_cu);
     }
 #endif
-    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, ctx->luma_lead, b->d_err, dbg);
+    const int lead = ctx->luma_lead >= 0 ? ctx->luma_lead : (alone ? 8 : 5);
+    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, lead, b->d_err, dbg);
     HIP_TRY(hipGetLastError());
 #ifdef P265R_DEBUG_DIAG
     if (dbg) {
