@@ -114,6 +114,37 @@ __device__ __forceinline__ int ang_inv(uint32_t angw) {
     return (int)((angw >> 8) & 0x1fffu);      // the angle tables store 256 for the modes without one
 }
 
+// AngTab4: the 4x4 angular table in LDS (35 modes x 16 samples, one dword each; modes 0 / 1 zero).
+// Entry of mode m, sample (x, y) of a 4x4 block: byte 0 / 1 = 4 x the linear reference index of
+// the two samples 8.4.4.2.6 interpolates (ds_bpermute byte addresses), byte 2 = iFact, byte 3 =
+// 32 - iFact.  Quad stages read their sample's entry with the stage's gather, so an angular stage
+// costs two bpermutes and the weighting instead of the projection arithmetic.
+// AngTab8 (P265R_ANGTAB8): the same for 8x8 blocks (35 x 64 dwords), read by the fast luma 8x8
+// and Cb+Cr 8x8 jobs.
+#ifndef P265R_ANGTAB8
+#define P265R_ANGTAB8 0
+#endif
+constexpr int kAngTab4Bytes = 35 * 16 * 4;
+constexpr int kAngTab8Bytes = P265R_ANGTAB8 ? 35 * 64 * 4 : 0;
+constexpr int kAngTabBytes = kAngTab4Bytes + kAngTab8Bytes;
+template <int LOG2>
+__device__ __forceinline__ uint32_t angtab_entry(int m, int p) {
+    constexpr int n = 1 << LOG2;
+    if (m < 2) return 0u;
+    const int x = p & (n - 1), y = p >> LOG2;
+    const int ang = c_angle[m];
+    const int ia = c_inv_angle[m] ? -(int)c_inv_angle[m] : 256;
+    const bool vert = m >= 18;
+    const int ns = vert ? -1 : 1;
+    const int along = vert ? y : x, across = vert ? x : y;
+    const int pa = (along + 1) * ang;
+    const int idx = pa >> 5, fact = pa & 31;
+    const int nr0 = -1 - across - idx;
+    auto ref = [&](int nr) { return 2 * n + ns * max(nr, (nr * ia + 128) >> 8); };   // ang_ref<2n>
+    const uint32_t a = (uint32_t)(ref(nr0) * 4) & 0xffu, b = (uint32_t)(ref(nr0 - 1) * 4) & 0xffu;
+    return a | b << 8 | (uint32_t)fact << 16 | (uint32_t)(32 - fact) << 24;
+}
+
 struct WaveLds {                 // one wave's private CTU state (4432 B): a wave holds one row
     uint8_t  ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
     union {                      // ref: raw / final linear reference arrays (8-bit samples)
@@ -149,7 +180,7 @@ struct RowCtrl {                 // 256 B at the start of dynamic LDS
 // dequeued, and at every row start runs at priority 1 while it is behind its partner.
 constexpr int kRowCuSlots = 2048;
 struct RowCuSlot { int count; int prog[3]; };
-// Dynamic LDS layout: [RowCtrl 256 B][prog: fs x hc ints][W x WaveLds][fs x 2 line buffers]
+// Dynamic LDS layout: [RowCtrl 256 B][prog: fs x hc ints][W x WaveLds][fs x 2 line buffers][AngTab4][AngTab8]
 // prog[slot][cy] = (local picture index & 0xffff) << 16 | CTUs done.
 
 __device__ __forceinline__ void wave_sync() {
@@ -374,7 +405,9 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 // Prediction (8.4.4.2.4-6) of sample (x, y) of a fast job: lane k of v holds reference
 // sample k of this lane's half (linear order of 8.4.4.2.2, substituted, filtered);
 // angw = intraPredAngle (int8, bits 0..7) | |invAngle| << 8 (job word w1's layout; 256 without one).
-template <int LOG2, bool PAIR>
+// TAB: angw is instead this lane's entry of the workgroup's 4x4 angular table (AngTab4: both
+// reference indices and the weights, no projection arithmetic); modes 10 / 26 are told by number.
+template <int LOG2, bool PAIR, bool TAB = false>
 __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, int y, int k, int hl, int half) {
     constexpr int n = 1 << LOG2;
     constexpr int maxv = 255;
@@ -404,7 +437,7 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
             const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
             pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
         }
-    } else if (P265R_HV_FAST && (angw & 0xffu) == 0u) {
+    } else if (P265R_HV_FAST && (TAB ? (mode & ~16) == 10 : (angw & 0xffu) == 0u)) {
         // modes 10 / 26 (intraPredAngle 0): a copy of the column left / the row above, plus the
         // luma boundary smoothing of 8.4.4.2.6 (fast jobs are n < 32) - no projection arithmetic
         const bool vert = mode >= 18;
@@ -414,6 +447,10 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
             const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
             pred = (vert ? x : y) == 0 ? edge : pred;
         }
+    } else if (TAB) {
+        const int a = __builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), v);
+        const int b = __builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), v);
+        pred = (__mul24((int)(angw >> 24), a) + __mul24((int)((angw >> 16) & 0xffu), b) + 16) >> 5;
     } else {
         const int ang = (int)(int8_t)(angw & 0xffu);
         const int ia = ang_inv(angw);
@@ -445,7 +482,7 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
 // lane's residual sample as loaded (ignored when the TB has none).
 template <int LOG2, bool PAIR>
 __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1,
-                                           uint32_t w5, int r16, int lane) {
+                                           uint32_t w5, int r16, int lane, uint32_t tab) {
     constexpr int n = 1 << LOG2;
     constexpr int nn = n * n;
     constexpr int maxv = 255;
@@ -472,6 +509,14 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     const int th = 2 * n + (yr > 0 ? 1 : 0);
     const uint32_t sa = tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
     const int raw = (int)*lds8(sa);
+    // luma: this sample's angular table entry (AngTab4 / AngTab8), read together with the gather
+    constexpr bool TAB = !PAIR && (LOG2 == 2 || (LOG2 == 3 && P265R_ANGTAB8));
+    uint32_t te = w1;
+    if constexpr (TAB) {
+        const uint32_t t0 = tab + (LOG2 == 3 ? (uint32_t)kAngTab4Bytes : 0u);
+        te = *lds32(t0 + (uint32_t)mode * (uint32_t)(nn * 4) + (uint32_t)((hl & (nn - 1)) * 4));
+        asm volatile("" : "+v"(te));
+    }
     int v = (w0 & J_NONE) ? 128 : raw;
     if (!PAIR && LOG2 == 3 && ((w0 >> 24) & 3u)) {           // [1 2 1] (8.4.4.2.3), 8x8: never strong
         const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
@@ -482,7 +527,7 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------------------
     const int sidx = hl < nn ? hl : 0;
     const int x = sidx & (n - 1), y = sidx >> LOG2;
-    const int pred = fast_pred<LOG2, PAIR>(mode, w1, v, x, y, k, hl, half);
+    const int pred = fast_pred<LOG2, PAIR, TAB>(mode, te, v, x, y, k, hl, half);
     // every lane stores (no exec-mask juggling): lanes without a sample of this job write a
     // private byte of the (here unused) reference scratch area
     const bool own = hl < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
@@ -612,7 +657,7 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
 // below 2^16 per half (planar / DC 2n x 255 + n, angular 32 x 255 + 16), so the halves never
 // carry into each other and one shift + mask divides both.  Lane k of v holds reference k of
 // 8.4.4.2.2's linear order.  Chroma (4:2:0) has no DC / horizontal / vertical boundary smoothing.
-template <int LOG2>
+template <int LOG2, bool TAB = false>
 __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, int x, int y, int k) {
     constexpr int n = 1 << LOG2;
     constexpr uint32_t rnd = (uint32_t)n * 0x00010001u;
@@ -629,6 +674,11 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
         const uint32_t s = (uint32_t)wave_sum<false, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>(in ? (int)v : 0, 0) + rnd;
         return (s >> (LOG2 + 1)) & msk;
+    }
+    if (TAB) {                                                 // AngTab4 entry (modes 10 / 26 included: fact 0)
+        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), (int)v);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), (int)v);
+        return ((__umul24(angw >> 24, a) + __umul24((angw >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
     }
     if (P265R_HV_FAST && (angw & 0xffu) == 0u)                  // modes 10 / 26: a copy (no chroma smoothing)
         return ref(mode >= 18 ? 2 * n + 1 + x : 2 * n - 1 - y);
@@ -658,7 +708,7 @@ __device__ __forceinline__ uint32_t cquad_recon(uint32_t pred, uint32_t res) {
 // (l & 7, l >> 3) of both.  r32 = this lane's residual pair Cb | Cr << 16; line_cb = the row
 // above the CTU in the Cb line buffer.
 __device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, uint32_t cw, uint32_t w0, uint32_t w1,
-                                             uint32_t w5, int r32, int lane) {
+                                             uint32_t w5, int r32, int lane, uint32_t tab) {
     constexpr int n = 8, ist = 32;
     const int ofs = (int)(w0 & 0x1fffu);
     const int xr = (ofs - 4096) & 31, yr = (ofs - 4096) >> 5;
@@ -676,9 +726,14 @@ __device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, u
     const uint32_t sa = tb + sref + (left ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
     const uint32_t dcr = left ? (xr == 0 ? 32u : 1024u) : (yr == 0 ? cw : 1024u);
     const uint32_t cb = *lds8(sa), cr = *lds8(sa + dcr);
+    uint32_t te = w1;
+    if constexpr (P265R_ANGTAB8) {                            // AngTab8 entry of sample lane
+        te = *lds32(tab + (uint32_t)kAngTab4Bytes + (uint32_t)mode * 256u + (uint32_t)lane * 4u);
+        asm volatile("" : "+v"(te));
+    }
     const uint32_t v = (w0 & J_NONE) ? 0x00800080u : (cb | cr << 16);
     const int x = lane & 7, y = lane >> 3;
-    const uint32_t rec = cquad_recon(cpred<3>(mode, w1, v, x, y, k), (uint32_t)r32);
+    const uint32_t rec = cquad_recon(cpred<3, (bool)P265R_ANGTAB8>(mode, te, v, x, y, k), (uint32_t)r32);
     const uint32_t da = orgA + (uint32_t)(y * ist + x);
     *lds8(da) = (uint8_t)rec;
     *lds8(da + 1024) = (uint8_t)(rec >> 16);
@@ -693,7 +748,7 @@ __device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, u
 // reconstruct their sample into rec.  CH: chroma quad, every value a packed Cb | Cr << 16 pair.
 template <int Q, bool CH>
 __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, bool none, int fa, int la,
-                                          uint32_t angw, int r16, int qid, int xs, int ys) {
+                                          uint32_t te, int r16, int qid, int xs, int ys) {
     constexpr int maxv = 255;
     const int s = min(max(lane, fa), la);                        // substituted reference index
     auto bp = [](int i, int src) { return __builtin_amdgcn_ds_bpermute(i << 2, src); };
@@ -711,11 +766,11 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     }
     if constexpr (CH) {
         v = none ? 0x00800080 : v;
-        const int rq = (int)cquad_recon(cpred<2>(mode, angw, (uint32_t)v, xs, ys, lane), (uint32_t)r16);
+        const int rq = (int)cquad_recon(cpred<2, true>(mode, te, (uint32_t)v, xs, ys, lane), (uint32_t)r16);
         return qid == Q ? rq : rec;
     } else {
         v = none ? 128 : v;
-        const int rq = clip_pel(fast_pred<2, false>(mode, angw, v, xs, ys, lane, lane, 0) + r16, maxv);
+        const int rq = clip_pel(fast_pred<2, false, true>(mode, te, v, xs, ys, lane, lane, 0) + r16, maxv);
         return qid == Q ? rq : rec;
     }
 }
@@ -730,7 +785,7 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
 // for this lane's component (chroma: lane half 0 Cb, 1 Cr).
 template <bool CH>
 __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1, uint32_t w2,
-                                           int angtab, int r16, int lane) {
+                                           uint32_t tab, int r16, int lane) {
     constexpr int ist = CH ? 32 : 64, last = ist - 1;           // interior stride, last row / column
     const int ofs = (int)(w0 & 0x1fffu);
     const int X = CH ? ((ofs - 4096) & 31) : (ofs & 63), Y = CH ? ((ofs - 4096) >> 5) : (ofs >> 6);
@@ -749,7 +804,10 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     if constexpr (CH) ext |= __builtin_amdgcn_ds_bpermute(((lane + 32) & 63) << 2, ext) << 16;   // Cb | Cr << 16
     const int xs = lane & 3, ys = (lane >> 3) & 3;
     const int qid = ((lane >> 4) & 2) | ((lane >> 2) & 1);
-    auto ang = [&](uint32_t m) { return (uint32_t)__builtin_amdgcn_readlane(angtab, (int)m); };
+    // this lane's AngTab4 entry of mode m (sample (xs, ys) of its sub-TB), read with the stage's gather
+    const uint32_t pos4 = (uint32_t)((ys * 4 + xs) * 4);
+    // (pinned at the stage start: the read then shares the gather's LDS wait instead of adding one)
+    auto ang = [&](uint32_t m) { uint32_t te = *lds32(tab + m * 64u + pos4); asm volatile("" : "+v"(te)); return te; };
     int rec = 0;
     {
         const uint32_t m = (w0 >> 17) & 63u;
@@ -807,8 +865,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
     unsigned char* lines = smem + 256 + prog_bytes + W * sizeof(WaveLds);
 
-    // intraPredAngle | |invAngle| << 8 (256 without one) of mode m in lane m (quad jobs read theirs with v_readlane)
-    const int angtab = lane < 35 ? (int)((uint32_t)(uint8_t)c_angle[lane] | (uint32_t)(c_inv_angle[lane] ? -(int)c_inv_angle[lane] : 256) << 8) : 0;
+    uint32_t* const atab = reinterpret_cast<uint32_t*>(lines + (size_t)fs_count * 2 * line_bytes);   // AngTab4
     if (threadIdx.x == 0) {
         ctl.next_row = 0; ctl.error = 0;
         ctl.cu_slot = -1; ctl.cu_rank = 0;
@@ -827,6 +884,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     if (threadIdx.x < 28) ctl.pad[threadIdx.x] = 0;
 #endif
     for (int i = threadIdx.x; i < fs_count * units; i += 64 * W) prog[i] = -1;
+    for (int i = threadIdx.x; i < 35 * 16; i += 64 * W) atab[i] = angtab_entry<2>(i >> 4, i & 15);
+    if (P265R_ANGTAB8)
+        for (int i = threadIdx.x; i < 35 * 64; i += 64 * W) atab[35 * 16 + i] = angtab_entry<3>(i >> 6, i & 63);
     __syncthreads();
 
     const int G = gridDim.x;
@@ -1038,8 +1098,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 // (7 inlined instances would otherwise hold them all live: ~150 VGPRs).
                 int ln;
                 asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-                uint32_t lbase, tl, tc, tcb;
+                uint32_t lbase, tl, tc, tcb, tab;
                 asm volatile("s_mov_b32 %0, %1" : "=s"(lbase) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&L)));
+                asm volatile("s_mov_b32 %0, %1" : "=s"(tab) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)atab)));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"((uint32_t)(uintptr_t)ltop_l));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tc) : "v"((uint32_t)(uintptr_t)ltop_c));
                 asm volatile("s_mov_b32 %0, %1" : "=s"(tcb) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ltop_cb)));
@@ -1047,15 +1108,15 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_QUAD) {
-                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tc, w0, w1, w2, angtab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
-                    else recon_quad<false>(lbase, tl, w0, w1, w2, angtab, c16, ln);
+                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tc, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
+                    else recon_quad<false>(lbase, tl, w0, w1, w2, tab, c16, ln);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
-                        case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln); break;
-                        case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln); break;
+                        case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;
+                        case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;
                         case 2: recon_fast16(lbase, tl, w0, w1, w5, make_uint4((uint32_t)c16, (uint32_t)c16m, 0u, 0u), ln); break;
-                        case 5: recon_cfast8(lbase, tcb, (uint32_t)g.cw, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln); break;
-                        default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln); break;
+                        case 5: recon_cfast8(lbase, tcb, (uint32_t)g.cw, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, tab); break;
+                        default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln, tab); break;
                     }
                 } else {
                   const uint4* ra_p = res_addr(w0, w3, w4);

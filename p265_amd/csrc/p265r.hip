@@ -270,7 +270,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     // complete (the kernel waits for that, so fewer slots would still be correct)
     int fs = std::min(32, (W + 2 * g.hc - 1) / (2 * g.hc) + 1);     // 2 row units (luma, chroma) per CTU row
     auto lds_of = [&](int f) {
-        return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw);
+        return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw) +
+               kAngTabBytes;
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
     auto fn = intra_rows_kernel<W, WPE>;

@@ -11,17 +11,17 @@ __global__ __launch_bounds__(64) void probe(const uint32_t* __restrict__ w, int 
     extern __shared__ unsigned char smem[];
     const int lane = threadIdx.x;
     const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
-    const int angtab = (int)w[lane];
+    const uint32_t tab = lbase + 8192u;   // AngTab4 stand-in
     for (int t = 0; t < n; ++t) {
         const uint32_t w0 = __builtin_amdgcn_readfirstlane(w[8 * t]), w1 = __builtin_amdgcn_readfirstlane(w[8 * t + 1]);
         const uint32_t w2 = __builtin_amdgcn_readfirstlane(w[8 * t + 2]), w5 = __builtin_amdgcn_readfirstlane(w[8 * t + 3]);
         const int r16 = (int)w[8 * t + 64 + lane];
 #if PROBE == 0
-        recon_quad<false>(lbase, lt, w0, w1, w2, angtab, r16, lane);
+        recon_quad<false>(lbase, lt, w0, w1, w2, tab, r16, lane);
 #elif PROBE == 1
-        recon_quad<true>(lbase, lt, w0, w1, w2, angtab, r16, lane);
+        recon_quad<true>(lbase, lt, w0, w1, w2, tab, r16, lane);
 #elif PROBE == 2
-        recon_fast<3, false>(lbase, lt, w0, w1, w5, r16, lane);
+        recon_fast<3, false>(lbase, lt, w0, w1, w5, r16, lane, tab);
 #else
         recon_fast16(lbase, lt, w0, w1, w5, make_uint4(r16, r16, 0, 0), lane);
 #endif
