@@ -122,7 +122,7 @@ __device__ __forceinline__ int ang_inv(uint32_t angw) {
 // AngTab8 (P265R_ANGTAB8): the same for 8x8 blocks (35 x 64 dwords), read by the fast luma 8x8
 // and Cb+Cr 8x8 jobs.
 #ifndef P265R_ANGTAB8
-#define P265R_ANGTAB8 0
+#define P265R_ANGTAB8 1
 #endif
 constexpr int kAngTab4Bytes = 35 * 16 * 4;
 constexpr int kAngTab8Bytes = P265R_ANGTAB8 ? 35 * 64 * 4 : 0;

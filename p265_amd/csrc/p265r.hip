@@ -101,6 +101,7 @@ struct p265r_ctx {
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
                                // 45.5/44.9/44.4/44.7 M CTU/s; round 1, W=8: lead 0/1/2/3/5/8/17 ->
                                // 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
+    int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (P265R_PIPE_WAVES 4, 6, 8)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every phase (P265R_DEBUG_DIAG
                                // builds also trace the row kernel's waves and print placement statistics)
@@ -321,6 +322,8 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     switch (ctx->row_waves) {
         case 0:
             if (alone) return launch_rows_w<12, 6>(ctx, b, st, alone);
+            if (ctx->pipe_waves == 4) return launch_rows_w<4, 1>(ctx, b, st, alone);
+            if (ctx->pipe_waves == 6) return launch_rows_w<6, 1>(ctx, b, st, alone);
             return launch_rows_w<8, 6>(ctx, b, st, alone);
         case 4: return launch_rows_w<4, 1>(ctx, b, st, alone);
         case 6: return launch_rows_w<6, 1>(ctx, b, st, alone);
@@ -397,7 +400,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     // experiment / test knobs read from the environment (bench.py refuses to run with any set)
     for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_DEBUG_SYNC", "P265R_SAO_ROWS", "P265R_SKIP",
-                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES", "P265R_FORK_PREP"})
+                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES", "P265R_FORK_PREP", "P265R_PIPE_WAVES"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
@@ -405,7 +408,11 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
     if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
-    if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::atoi(v) != 0;
+    if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::min(2, std::max(0, std::atoi(v)));
+    if (const char* v = std::getenv("P265R_PIPE_WAVES")) {
+        const int w = std::atoi(v);
+        if (w == 4 || w == 6 || w == 8) ctx->pipe_waves = w;
+    }
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 16) ctx->row_waves = w;
@@ -729,7 +736,9 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     const bool prep = recon && ctx->schedule == 1 && !(skip & 2);
     hipStream_t ps = s;                              // the prep kernel's stream
     if (prep && ctx->fork_prep) {
-        const size_t li = (size_t)b->lane;
+        // fork_prep 2: one prep stream shared by all lanes (fewer streams than HW queues, so no
+        // lane's intra kernel sits in front of a prep kernel in a shared hardware queue)
+        const size_t li = ctx->fork_prep == 2 ? 0 : (size_t)b->lane;
         if (ctx->aux.size() <= li) {
             ctx->aux.resize(li + 1, nullptr); ctx->fork_ev.resize(li + 1, nullptr); ctx->join_ev.resize(li + 1, nullptr);
         }
@@ -748,7 +757,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         // waves start before the residual kernels fill the chip
         intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, 0, ps>>>(b->d_pics, g, b->view);
         ++tm.residual_launches;
-        if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[(size_t)b->lane], ps));
+        if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], ps));
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
         residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl);
@@ -774,7 +783,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[(size_t)b->lane], 0));
+    if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], 0));
     if (b->dbk) {
         // deblocking edge / QpY map: depends on the records only
         dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
@@ -959,11 +968,11 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
     const int n = snprintf(tmp, sizeof(tmp),
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
-        "\"pipeline\": %d, \"fork_prep\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
+        "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
-        ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, W=8 register-lean while other lanes have work",
+        ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, pipe_waves while other lanes have work",
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
-        ctx->pipeline, ctx->fork_prep, ctx->num_cus,
+        ctx->pipeline, ctx->fork_prep, ctx->pipe_waves, ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG
         1,
 #else
