@@ -163,6 +163,17 @@ __device__ __forceinline__ bool tb_same_tu_chroma(const p265r_tb& cb, const p265
            cb.pred_mode == cr.pred_mode && ((cb.flags ^ cr.flags) & P265R_TB_PCM) == 0;
 }
 
+// Global-address-space (not flat) accesses for the prep kernel: a flat load or store also counts
+// in lgkmcnt, so every LDS wait of the kernel would wait for the outstanding HBM traffic too.
+typedef unsigned int prep_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 prep_ld16(const void* p) {
+    const prep_u4 v = *(const __attribute__((address_space(1))) prep_u4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void prep_st16(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    *(__attribute__((address_space(1))) prep_u4*)p = prep_u4{a, b, c, d};
+}
+
 // grid (CTUs, pictures), 64 threads: one wave per CTU walks its TBs 64 at a time.  A CTU's
 // job list is [chroma jobs][luma jobs]; both are staged in LDS (luma words 0, 1, 2, 3, 5, at
 // most 256 jobs per CTU; chroma words 0..5, at most 128; p265r.hip validate_picture) so that
@@ -176,9 +187,10 @@ __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_
     J.w[4] = zero_off; J.w[5] = l.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
     return J;
 }
-// job word w1 of a staged job: intraPredAngle | |invAngle| << 8 (c_angw), availability bit 32 << 21
-__device__ __forceinline__ uint32_t job_w1(uint32_t w0, uint32_t w5) {
-    return c_angw[(w0 >> 17) & 63u] | ((w5 & kJ5Bit32) ? 1u << 21 : 0u);
+// job word w1 of a staged job: intraPredAngle | |invAngle| << 8 (c_angw), availability bit 32 << 21;
+// angv = c_angw[lane] (lanes 0..34), picked per lane with a bpermute instead of a global load
+__device__ __forceinline__ uint32_t job_w1(uint32_t w0, uint32_t w5, uint32_t angv) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((w0 >> 17) & 63u) << 2), (int)angv) | ((w5 & kJ5Bit32) ? 1u << 21 : 0u);
 }
 // grid (wc, hc, pictures), one 64-thread wave per CTU
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g, BatchView v) {
@@ -190,6 +202,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const int cx = blockIdx.x, cy = blockIdx.y;
     const int addr = cy * g.wc + cx;
     const int lane = threadIdx.x;
+    const uint32_t angv = lane < 35 ? c_angw[lane] : 0u;
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
     // this CTU's record and its left / top / top-left / top-right neighbours' first 16 B (slice,
@@ -228,7 +241,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
 #pragma unroll
     for (int i = 0; i < kPrepChunks; ++i) {
         const int t = i * 64 + lane;
-        rv[i] = t < cnt ? tv[t] : make_uint4(0u, 0u, 0u, 0u);
+        rv[i] = t < cnt ? prep_ld16(tv + t) : make_uint4(0u, 0u, 0u, 0u);
     }
     auto from_prev_lane = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false); };
     auto from_next_lane = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false); };
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         hp = H;
         const unsigned long long me_ = __ballot(emit);
         const ChromaJobLds c = sc[s1];
-        const uint32_t w1 = job_w1(c.w0, c.w5);
+        const uint32_t w1 = job_w1(c.w0, c.w5, angv);
         IntraJob J;
         if (hd) {
             J = make_cquad(sc + sq, qb, qc, P.zero_off);
@@ -359,8 +372,8 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         }
         if (emit) {
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + rank(me_));
-            dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
-            dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
+            prep_st16(dst, J.w[0], J.w[1], J.w[2], J.w[3]);
+            prep_st16(dst + 1, J.w[4], J.w[5], J.w[6], J.w[7]);
         }
         c_out += __popcll(me_);
     }
@@ -376,16 +389,16 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         hp = H;
         const unsigned long long me_ = __ballot(emit);
         const LumaJobLds l = sj[s1];
-        const uint32_t w1 = job_w1(l.w0, l.w5);
+        const uint32_t w1 = job_w1(l.w0, l.w5, angv);
         const IntraJob J = hd ? make_quad(sj + sq) : luma_job(l, P.zero_off, w1);
         if (emit) {
             uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + n_out + rank(me_));
-            dst[0] = make_uint4(J.w[0], J.w[1], J.w[2], J.w[3]);
-            dst[1] = make_uint4(J.w[4], J.w[5], J.w[6], J.w[7]);
+            prep_st16(dst, J.w[0], J.w[1], J.w[2], J.w[3]);
+            prep_st16(dst + 1, J.w[4], J.w[5], J.w[6], J.w[7]);
         }
         n_out += __popcll(me_);
     }
-    if (lane == 0) P.jcount[addr] = (uint32_t)n_out | (uint32_t)c_out << 16;
+    if (lane == 0) *(__attribute__((address_space(1))) uint32_t*)(P.jcount + addr) = (uint32_t)n_out | (uint32_t)c_out << 16;
 }
 
 }  // namespace p265r

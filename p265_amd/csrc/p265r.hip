@@ -961,6 +961,12 @@ int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
     return P265R_OK;
 }
 
+// GPU_MAX_HW_QUEUES as the HIP runtime read it at initialisation (HIP's default 4 when unset)
+static const char* hwq_env() {
+    const char* v = std::getenv("GPU_MAX_HW_QUEUES");
+    return (v && std::strlen(v) < 8 && std::strspn(v, "0123456789") == std::strlen(v)) ? v : "default";
+}
+
 int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
     if (!ctx || size < 0 || (size > 0 && !buf)) return P265R_EINVAL;
     const Geo& g = ctx->geo;
@@ -968,11 +974,12 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
     const int n = snprintf(tmp, sizeof(tmp),
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
-        "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"num_cus\": %d, \"diag_build\": %d, \"env_overrides\": [%s]}",
+        "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
+        "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, pipe_waves while other lanes have work",
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
-        ctx->pipeline, ctx->fork_prep, ctx->pipe_waves, ctx->num_cus,
+        ctx->pipeline, ctx->fork_prep, ctx->pipe_waves, hwq_env(), ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG
         1,
 #else
