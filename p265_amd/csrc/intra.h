@@ -76,6 +76,7 @@ __constant__ int16_t c_inv_angle[35];
 // job word w1 of mode m (intra_prep.h): intraPredAngle (int8) | |invAngle| << 8 (256 for the modes
 // without an inverse angle: intra_rows.h ang_inv)
 __constant__ uint32_t c_angw[35];
+__constant__ uint32_t c_ztab[64];       // avail_ztab_word(s, yu) at 16 s + yu (ref_avail_mask32)
 
 __host__ __device__ __forceinline__ int morton4(int x, int y) {      // 4-bit x, y -> 8-bit z-order
     x = (x | (x << 2)) & 0x33; x = (x | (x << 1)) & 0x55;
@@ -160,6 +161,49 @@ __host__ __device__ __forceinline__ unsigned long long ref_avail_mask(int c, int
     const unsigned long long m_t = bits(L + 1, L + 1 + half);
     const unsigned long long m_tr = bits(L + 1 + half, L + 1 + max(half, min(L, j_max)));
     return (bl ? m_bl : 0ull) | (left ? m_l : 0ull) | (corner ? m_c : 0ull) | (top ? m_t : 0ull) | (tr ? m_tr : 0ull);
+}
+
+// z-order availability of the bottom-left / top-right neighbour unit inside the CTB (the morton
+// comparisons of ref_avail_mask), tabulated: word 16 s + yu for TBs of 4 << s luma samples
+// (s = 0..3) in unit row yu; bit 2 xu: unit (xu - 1, yu + 2^s) precedes unit (xu, yu) in z-order,
+// bit 2 xu + 1: unit (xu + 2^s, yu - 1) does.  Independent of the CTB size: z-order of 4x4 units
+// inside any aligned square; the cases at the CTB's edges are decided before the table is read.
+__host__ __device__ inline uint32_t avail_ztab_word(int s, int yu) {
+    const int su = 1 << s;
+    uint32_t w = 0;
+    for (int xu = 0; xu < 16; ++xu) {
+        const int zc = morton4(xu, yu);
+        if (xu > 0 && yu + su < 16 && morton4(xu - 1, yu + su) < zc) w |= 1u << (2 * xu);
+        if (yu > 0 && xu + su < 16 && morton4(xu + su, yu - 1) < zc) w |= 1u << (2 * xu + 1);
+    }
+    return w;
+}
+
+// ref_avail_mask in 32-bit pieces: returns units 0..31, bit32 = unit 32 (only a 32-sample luma /
+// 16-sample chroma TB has it), with the z-order comparisons read from zw = avail_ztab_word(log2(n
+// in luma samples) - 2, yc / 4).  Equal to ref_avail_mask (tools/avail_check.hip, exhaustive).
+__host__ __device__ __forceinline__ uint32_t ref_avail_mask32(int c, int xr, int yr, int n, int x0, int y0, int w,
+                                                              int h, int ctb, unsigned flags, uint32_t zw,
+                                                              uint32_t& bit32) {
+    const int sub = c ? 1 : 0;
+    const int xc = xr << sub, yc = yr << sub, nl = n << sub;      // luma, CTB-relative
+    const int L = nl >> 1, half = L >> 1;                         // units (4 luma samples) per side
+    const int xu = (xc >> 2) & 15;
+    const bool fl = (flags & 1u) != 0, ft = (flags & 2u) != 0, ftl = (flags & 4u) != 0, ftr = (flags & 8u) != 0;
+    const bool left = (xc > 0) | fl;
+    const bool bl = (yc + nl < ctb) & (xc == 0 ? fl : ((zw >> (2 * xu)) & 1u) != 0);
+    const bool corner = xc > 0 ? ((yc > 0) | ft) : (yc > 0 ? fl : ftl);
+    const bool top = (yc > 0) | ft;
+    const bool tr = xc + nl < ctb ? (yc > 0 ? ((zw >> (2 * xu + 1)) & 1u) != 0 : ft) : ((yc == 0) & ftr);
+    const int u_min = max(0, (y0 + yc + 2 * nl - h) >> 2);        // units below the picture: u < u_min
+    const int j_max = (w - x0 - xc) >> 2;                          // top units inside the picture: j < j_max
+    auto bits = [](int lo, int wd) -> uint32_t { return ((1u << wd) - 1u) << lo; };   // lo <= 25, wd <= 16
+    const uint32_t m_bl = bits(min(u_min, half), max(half - u_min, 0)), m_l = bits(half, half), m_c = 1u << L;
+    const uint32_t m_t = bits(L + 1, half);
+    const int tr_w = max(min(L, j_max) - half, 0);
+    const uint32_t m_tr = bits(L + 1 + half, min(tr_w, 31 - (L + half)));   // the part below bit 32
+    bit32 = (tr & (L == 16) & (j_max >= 16)) ? 1u : 0u;
+    return (bl ? m_bl : 0u) | (left ? m_l : 0u) | (corner ? m_c : 0u) | (top ? m_t : 0u) | (tr ? m_tr : 0u);
 }
 
 __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict__ pics,

@@ -203,6 +203,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const int addr = cy * g.wc + cx;
     const int lane = threadIdx.x;
     const uint32_t angv = lane < 35 ? c_angw[lane] : 0u;
+    const uint32_t ztv = c_ztab[lane];                            // avail_ztab_word(lane >> 4, lane & 15)
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
     // this CTU's record and its left / top / top-left / top-right neighbours' first 16 B (slice,
@@ -298,8 +299,13 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const int mode = rec.pred_mode;
             // ---- availability per reference unit, linear order (8.4.4.2.2) -----------------
             const int L = (2 * n) >> (c ? 1 : 2);
-            const unsigned long long m = ref_avail_mask(c, xr, yr, n, x0, y0, g.w, g.h, ctb, flags);
-            const unsigned long long full = (1ull << (2 * L + 1)) - 1ull;
+            // z-order word of the TB's size and unit row (ztv: lane i holds avail_ztab_word word i)
+            const int zs = (31 - __clz(n)) + sub - 2, yu = (yr << sub) >> 2;
+            const uint32_t zw = (uint32_t)__builtin_amdgcn_ds_bpermute((zs * 16 + yu) << 2, (int)ztv);
+            uint32_t mhi;
+            const uint32_t mlo = ref_avail_mask32(c, xr, yr, n, x0, y0, g.w, g.h, ctb, flags, zw, mhi);
+            const uint32_t full_lo = L == 16 ? 0xffffffffu : (1u << (2 * L + 1)) - 1u;
+            const bool m_full = (mlo == full_lo) & (mhi == (L == 16 ? 1u : 0u)), m_none = (mlo | mhi) == 0u;
             // ---- filtering decision (8.4.4.2.3), luma only in 4:2:0 ---------------------------
             const int dist = min(abs(mode - 26), abs(mode - 10));
             const bool fon = (c == 0) & (n != 4) & (mode != 1) & (dist > (n == 8 ? 7 : (n == 16 ? 1 : 0)));
@@ -318,22 +324,23 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             const uint32_t off1 = cm == 2 ? r0 : (pair ? roff(f1, next.coef_off) : P.zero_off);
             const uint32_t w0 = ofs | (uint32_t)(lg - 2) << 13 | cm << 15 | (uint32_t)mode << 17 |
                                 ((f0 & P265R_TB_PCM) ? J_PCM : 0u) | filt << 24 | raw(fh0) << 26 | raw(fh1) << 27 |
-                                coded(fh0) << 28 | coded(fh1) << 29 | (m == full ? J_ALL : 0u) | (m == 0 ? J_NONE : 0u);
-            const uint32_t w2 = (uint32_t)m;
+                                coded(fh0) << 28 | coded(fh1) << 29 | (m_full ? J_ALL : 0u) | (m_none ? J_NONE : 0u);
+            const uint32_t w2 = mlo;
             // fast path: one contiguous run of available units [ulo, uhi] -> sample bounds [fa, la]
 #ifndef P265R_FAST16
 #define P265R_FAST16 1
 #endif
             const bool fast_size = ((c == 0) & (n <= (P265R_FAST16 ? 16 : 8))) | ((cm == 3u) & (n <= (g.quad & 4 ? 4 : 8)));
             const int US = c ? 1 : 2;
-            const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);   // mhi: bit 32 only
             const int ulo = mlo ? __ffs((int)mlo) - 1 : 32;
             const int uhi = mhi ? 32 : 31 - __clz((int)(mlo | 1u));
-            const unsigned long long run = ((2ull << uhi) - 1ull) & ~((1ull << ulo) - 1ull);
+            // the available units form one run [ulo, uhi] (32-bit pieces; mhi = unit 32)
+            const uint32_t lo_cut = ulo >= 32 ? 0u : (0xffffffffu << ulo);
+            const bool contig = mlo == (mhi ? lo_cut : (lo_cut & (uhi >= 31 ? 0xffffffffu : ((2u << uhi) - 1u))));
             const int fa = ulo < L ? (ulo << US) : (ulo == L ? 2 * n : 2 * n + 1 + ((ulo - L - 1) << US));
             const int la = uhi < L ? ((uhi + 1) << US) - 1 : (uhi == L ? 2 * n : 2 * n + ((uhi - L) << US));
-            const bool fast = fast_size & !(f0 & P265R_TB_PCM) & ((m == 0) | (m == run));
-            const uint32_t w5 = !fast ? 0u : (m == 0 ? J5_FAST : (J5_FAST | (uint32_t)fa | (uint32_t)la << 8));
+            const bool fast = fast_size & !(f0 & P265R_TB_PCM) & (m_none | contig);
+            const uint32_t w5 = !fast ? 0u : (m_none ? J5_FAST : (J5_FAST | (uint32_t)fa | (uint32_t)la << 8));
             const uint32_t w5s = w5 | (mhi ? kJ5Bit32 : 0u);
             if (keep && kl) sj[slot] = LumaJobLds{w0, w2, off0, w5s};
             else if (keep && slot < kMaxCtuChroma) sc[slot] = ChromaJobLds{w0, w2, off0, off1, w5s};

@@ -329,6 +329,7 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
         case 6: return launch_rows_w<6, 1>(ctx, b, st, alone);
         case 10: return launch_rows_w<10, 5>(ctx, b, st, alone);
         case 12: return launch_rows_w<12, 6>(ctx, b, st, alone);
+        case 14: return launch_rows_w<14, 7>(ctx, b, st, alone);
         case 16: return launch_rows_w<16, 1>(ctx, b, st, alone);
         default:
             if (ctx->lean == 1 || (ctx->lean < 0 && !alone)) return launch_rows_w<8, 6>(ctx, b, st, alone);
@@ -415,7 +416,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     }
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
-        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 16) ctx->row_waves = w;
+        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16) ctx->row_waves = w;
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -430,6 +431,9 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
         e = hipMemcpyToSymbol(HIP_SYMBOL(c_angle), ang, sizeof(ang));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_inv_angle), inv, sizeof(inv));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_angw), angw, sizeof(angw));
+        uint32_t ztab[64];
+        for (int i = 0; i < 64; ++i) ztab[i] = avail_ztab_word(i >> 4, i & 15);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_ztab), ztab, sizeof(ztab));
     }
     if (e != hipSuccess) {
         int rc = hip_fail(e, "p265r_create");

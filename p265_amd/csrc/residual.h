@@ -36,7 +36,10 @@ __device__ __forceinline__ int clamp16i(int v) {
 }
 
 // d = Clip3(-32768, 32767, (L * 16 * levelScale[qP%6] << (qP/6) + (1 << (bdShift-1))) >> bdShift)
-// computed exactly in 32 bits: |L*16*72| < 2^31, and the shift pair is folded.
+// computed exactly in 32 bits with the shift pair folded: |L| <= 2^15 and 16 * 72 < 2^11 give
+// |L * scale| < 2^26 (one 24-bit multiply), and lshift = qP/6 - bdShift <= 8 - 5 = 3 (8-bit video:
+// qP <= 51, bdShift >= 5; p265r_create rejects other bit depths), so the shifted product stays
+// below 2^29.  (Round 2 widened it to 64 bits: ~10 VALU per coefficient instead of 5.)
 struct Dequant {
     int scale, lshift, rshift, rnd;
     __device__ __forceinline__ Dequant(int qp, int bd_shift) {
@@ -46,8 +49,8 @@ struct Dequant {
         else { lshift = 0; rshift = bd_shift - per; rnd = 1 << (rshift - 1); }
     }
     __device__ __forceinline__ int operator()(int level) const {
-        long long p = (long long)(level * scale);
-        return clamp16(((p << lshift) + rnd) >> rshift);
+        const int p = __mul24(level, scale);
+        return clamp16i(((p << lshift) + rnd) >> rshift);
     }
 };
 

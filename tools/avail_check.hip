@@ -5,7 +5,7 @@
 using namespace p265r;
 
 int main() {
-    long long checked = 0, bad = 0;
+    long long checked = 0, bad = 0, bad32 = 0;
     for (int ctb_log2 = 4; ctb_log2 <= 6; ++ctb_log2) {
         const int ctb = 1 << ctb_log2;
         for (int c = 0; c < 2; ++c)
@@ -34,6 +34,14 @@ int main() {
                                             ref |= 1ull << u;
                                     }
                                     const unsigned long long got = ref_avail_mask(c, xr, yr, n, x0, y0, w, h, ctb, flags);
+                                    uint32_t hi32 = 0;
+                                    const int s = __builtin_ctz((unsigned)(n << sub)) - 2;
+                                    const uint32_t lo32 = ref_avail_mask32(c, xr, yr, n, x0, y0, w, h, ctb, flags,
+                                                                           avail_ztab_word(s, yc >> 2), hi32);
+                                    const unsigned long long got32 = (unsigned long long)lo32 | (unsigned long long)hi32 << 32;
+                                    if (got32 != ref && bad32++ < 10)
+                                        printf("MISMATCH32 ctb %d c %d n %d xr %d yr %d flags %u w %d h %d: %llx vs %llx\n", ctb, c,
+                                               n, xr, yr, flags, w, h, got32, ref);
                                     ++checked;
                                     if (got != ref && bad++ < 10)
                                         printf("MISMATCH ctb %d c %d n %d xr %d yr %d flags %u w %d h %d: %llx vs %llx\n", ctb, c, n,
@@ -41,6 +49,6 @@ int main() {
                                 }
             }
     }
-    printf("checked %lld, mismatches %lld\n", checked, bad);
-    return bad ? 1 : 0;
+    printf("checked %lld, mismatches %lld\n", checked, bad + bad32);
+    return (bad + bad32) ? 1 : 0;
 }
