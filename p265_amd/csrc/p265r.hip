@@ -329,7 +329,6 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
         case 6: return launch_rows_w<6, 1>(ctx, b, st, alone);
         case 10: return launch_rows_w<10, 5>(ctx, b, st, alone);
         case 12: return launch_rows_w<12, 6>(ctx, b, st, alone);
-        case 14: return launch_rows_w<14, 7>(ctx, b, st, alone);
         case 16: return launch_rows_w<16, 1>(ctx, b, st, alone);
         default:
             if (ctx->lean == 1 || (ctx->lean < 0 && !alone)) return launch_rows_w<8, 6>(ctx, b, st, alone);
@@ -416,7 +415,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     }
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
-        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 14 || w == 16) ctx->row_waves = w;
+        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 16) ctx->row_waves = w;
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
