@@ -53,14 +53,17 @@ __device__ __forceinline__ void expand_mask(uint32_t m16, uint32_t* d) {
 }
 
 #ifndef P265R_SAO_WPE
-#define P265R_SAO_WPE 4
+#define P265R_SAO_WPE 6
 #endif
 
 constexpr int kSao16Strip = 62 * 16;       // output samples per strip
 #ifndef P265R_SAO16_CHUNK
-#define P265R_SAO16_CHUNK 4
+#define P265R_SAO16_CHUNK 2
 #endif
-constexpr int kSao16Chunk = P265R_SAO16_CHUNK;   // rows per load batch
+// rows per load batch: 2 (80 VGPRs, 6 waves per SIMD) rather than 4 (100 VGPRs): 0.74 -> 0.77 ms
+// alone, but two SAO waves per SIMD fit beside the W = 8 row kernel of another lane: pipelined
+// 46.9-47.1 -> 47.0-48.0 M CTU/s (3 interleaved reps, round 3)
+constexpr int kSao16Chunk = P265R_SAO16_CHUNK;
 
 // waves per picture: hc CTB rows x (luma strips + 2 x chroma strips)
 __host__ __device__ __forceinline__ int sao16_units(const Geo& g) {
