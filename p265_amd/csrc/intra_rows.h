@@ -428,11 +428,12 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
                 __mul24(y + 1, uref(n - 1)) + n) >> (LOG2 + 1);
     } else if (mode == 1) {
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
+        // luma: the edge samples' bpermutes go out first, their latency under the DPP reduction
+        const int lft = PAIR ? 0 : ref(2 * n - 1 - y), top = PAIR ? 0 : ref(2 * n + 1 + x);
         const int dc = (wave_sum<PAIR, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>((hl <= 4 * n && in) ? v : 0, half) + n) >> (LOG2 + 1);
         if (PAIR) {
             pred = dc;
         } else {                                                 // luma n < 32: edge smoothing
-            const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
             // (lft + 2dc + top + 2) >> 2 at (0,0); one-sided (3dc + side + 2) >> 2 on row 0 / column 0
             const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
             pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
@@ -778,20 +779,19 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
 // 4x4 QUAD job (J5_QUAD, intra_prep.h): the four fast 4x4 TBs of one 8x8 luma region (CH =
 // false), or the four Cb+Cr 4x4 pairs of one 8x8 chroma region (CH = true), in one job.  Lane
 // l = region sample (l & 7, l >> 3); the 25 external reference samples (column x = -1, rows
-// -1..11; row y = -1, columns 0..11) are read from LDS once (chroma: Cb by lanes 0-24, Cr by
-// lanes 32-56, then packed into lanes 0-24), the four stages pass their samples to each other
-// through registers (ds_bpermute), and the region is written to LDS once.  r16 = this lane's
-// residual sample (chroma: the packed Cb | Cr << 16 pair); line_top = the row above the CTU
-// for this lane's component (chroma: lane half 0 Cb, 1 Cr).
+// -1..11; row y = -1, columns 0..11) are read from LDS once (chroma: lanes 0-24 read the Cb sample
+// and its Cr twin, 1024 B further in the CTU interior, 32 B in the left column, cw B in the line
+// buffer, and pack them), the four stages pass their samples to each other through registers
+// (ds_bpermute), and the region is written to LDS once.  r16 = this lane's residual sample
+// (chroma: the packed Cb | Cr << 16 pair); line_top = the row above the CTU (chroma: the Cb line).
 template <bool CH>
-__device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1, uint32_t w2,
-                                           uint32_t tab, int r16, int lane) {
+__device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t cw, uint32_t w0, uint32_t w1,
+                                           uint32_t w2, uint32_t tab, int r16, int lane) {
     constexpr int ist = CH ? 32 : 64, last = ist - 1;           // interior stride, last row / column
     const int ofs = (int)(w0 & 0x1fffu);
     const int X = CH ? ((ofs - 4096) & 31) : (ofs & 63), Y = CH ? ((ofs - 4096) >> 5) : (ofs >> 6);
-    const int half = CH ? (lane >> 5) : 0;
-    const uint32_t orgA = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)(half * 1024);
-    const uint32_t leftA = lbase + (uint32_t)(CH ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft));
+    const uint32_t orgA = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs;
+    const uint32_t leftA = lbase + (uint32_t)(CH ? offsetof(WaveLds, cleft) : offsetof(WaveLds, yleft));
     // ---- external references: e = 0..12 column x = -1 (row e - 1), e = 13..24 row y = -1 ------
     const int e = min(CH ? (lane & 31) : lane, 24);
     // every candidate computed, then selected: no divergent branch per lane class
@@ -801,7 +801,10 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     const uint32_t row = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - ist + (uint32_t)min(c, last - X);
     const uint32_t ea = e > 12 ? row : (r < 0 ? line_top + (uint32_t)(X - 1) : col);
     int ext = (int)*lds8(ea);
-    if constexpr (CH) ext |= __builtin_amdgcn_ds_bpermute(((lane + 32) & 63) << 2, ext) << 16;   // Cb | Cr << 16
+    if constexpr (CH) {                                          // Cb | Cr << 16 (same LDS round trip)
+        const uint32_t dcr = e > 12 ? (Y == 0 ? cw : 1024u) : (r < 0 ? cw : (X > 0 ? 1024u : 32u));
+        ext |= (int)*lds8(ea + dcr) << 16;
+    }
     const int xs = lane & 3, ys = (lane >> 3) & 3;
     const int qid = ((lane >> 4) & 2) | ((lane >> 2) & 1);
     // this lane's AngTab4 entry of mode m (sample (xs, ys) of its sub-TB), read with the stage's gather
@@ -1108,8 +1111,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_QUAD) {
-                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tc, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
-                    else recon_quad<false>(lbase, tl, w0, w1, w2, tab, c16, ln);
+                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tcb, (uint32_t)g.cw, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
+                    else recon_quad<false>(lbase, tl, 0u, w0, w1, w2, tab, c16, ln);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
                         case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;

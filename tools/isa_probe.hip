@@ -17,9 +17,9 @@ __global__ __launch_bounds__(64) void probe(const uint32_t* __restrict__ w, int 
         const uint32_t w2 = __builtin_amdgcn_readfirstlane(w[8 * t + 2]), w5 = __builtin_amdgcn_readfirstlane(w[8 * t + 3]);
         const int r16 = (int)w[8 * t + 64 + lane];
 #if PROBE == 0
-        recon_quad<false>(lbase, lt, w0, w1, w2, tab, r16, lane);
+        recon_quad<false>(lbase, lt, 0u, w0, w1, w2, tab, r16, lane);
 #elif PROBE == 1
-        recon_quad<true>(lbase, lt, w0, w1, w2, tab, r16, lane);
+        recon_quad<true>(lbase, lt, 960u, w0, w1, w2, tab, r16, lane);
 #elif PROBE == 2
         recon_fast<3, false>(lbase, lt, w0, w1, w5, r16, lane, tab);
 #else
