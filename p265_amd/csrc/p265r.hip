@@ -101,6 +101,7 @@ struct p265r_ctx {
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
                                // 45.5/44.9/44.4/44.7 M CTU/s; round 1, W=8: lead 0/1/2/3/5/8/17 ->
                                // 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
+    bool stream_prio = false;  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
     int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (P265R_PIPE_WAVES 4, 6, 8)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every phase (P265R_DEBUG_DIAG
@@ -165,6 +166,16 @@ void parallel_for(int n, F fn) {
             for (int i; (i = next.fetch_add(1)) < n;) fn(i);
         });
     for (auto& t : th) t.join();
+}
+
+// a lane stream: default priority, or the device's highest with P265R_STREAM_PRIO (then the
+// dispatcher prefers the lanes' residual / intra / SAO workgroups over the prep streams')
+hipError_t lane_stream_create(const p265r_ctx* ctx, hipStream_t* st) {
+    if (!ctx->stream_prio) return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
 }
 
 int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
@@ -400,7 +411,8 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     // experiment / test knobs read from the environment (bench.py refuses to run with any set)
     for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_DEBUG_SYNC", "P265R_SAO_ROWS", "P265R_SKIP",
-                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES", "P265R_FORK_PREP", "P265R_PIPE_WAVES"})
+                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES", "P265R_FORK_PREP", "P265R_PIPE_WAVES",
+                          "P265R_STREAM_PRIO"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
@@ -419,7 +431,8 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (const char* v = std::getenv("P265R_STREAM_PRIO")) ctx->stream_prio = std::atoi(v) != 0;
+    if (e == hipSuccess) e = lane_stream_create(ctx, &ctx->stream);
     if (e == hipSuccess) ctx->lanes.push_back(ctx->stream);
     if (e == hipSuccess) {
         int8_t ang[35];
@@ -746,7 +759,13 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
             ctx->aux.resize(li + 1, nullptr); ctx->fork_ev.resize(li + 1, nullptr); ctx->join_ev.resize(li + 1, nullptr);
         }
         if (!ctx->aux[li]) {
-            HIP_TRY(hipStreamCreateWithFlags(&ctx->aux[li], hipStreamNonBlocking));
+            if (ctx->stream_prio) {
+                int least = 0, greatest = 0;
+                HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+                HIP_TRY(hipStreamCreateWithPriority(&ctx->aux[li], hipStreamNonBlocking, least));
+            } else {
+                HIP_TRY(hipStreamCreateWithFlags(&ctx->aux[li], hipStreamNonBlocking));
+            }
             HIP_TRY(hipEventCreateWithFlags(&ctx->fork_ev[li], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&ctx->join_ev[li], hipEventDisableTiming));
         }
@@ -956,7 +975,7 @@ int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
     HIP_TRY(hipSetDevice(ctx->device));
     while ((int)ctx->lanes.size() < depth) {
         hipStream_t st = nullptr;
-        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_TRY(lane_stream_create(ctx, &st));
         ctx->lanes.push_back(st);
     }
     ctx->pipeline = depth;
