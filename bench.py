@@ -29,6 +29,8 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -115,6 +117,10 @@ def parse():
                     help="deblocking on in every slice (real-stream config; SURVEY §8(d) defines the bench without it)")
     ap.add_argument("--experiment", action="store_true",
                     help="allow P265R_* library knobs in the environment (recorded in the line; not a headline run)")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="N > 1: control plane only, no RCCL communicator (ranks sharing one device: two RCCL "
+                         "ranks cannot); the params then travel over the control plane")
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-run output check (not a headline run)")
     return ap.parse_args()
 
 
@@ -196,6 +202,66 @@ def cpu_baseline(params, uniq, budget_s, threads, what):
     return {"value": round(ctus / dt, 1), "unit": "CTU/s", "cores": threads, "kind": "port",
             "sample": "oracle/recon_oracle.c (scalar C restatement, OpenMP over pictures): %d synthetic %s "
                       "= %d CTUs in %.1f s" % (n, what, ctus, dt)}
+
+
+def pictures_to_check(n, unique):
+    """Indices of a resident batch whose outputs are checked after the timed runs: the first and
+    the last ``unique`` pictures (every distinct synthetic picture, at both ends of the batch)."""
+    return sorted(set(range(min(unique, n))) | set(range(max(0, n - unique), n)))
+
+
+def sha_planes(planes):
+    import hashlib
+    return hashlib.sha256(b"".join(np.ascontiguousarray(p).tobytes() for p in planes)).hexdigest()
+
+
+def verify_planes(params, pics, got, threads):
+    """Compare downloaded planes with the C oracle (oracle/recon_oracle.c, the checker).
+
+    ``got``: {picture index: [Y, Cb, Cr]} for pictures of ``pics``; identical Picture objects
+    (the replicated synthetic pictures) are decoded once.  -> (n_checked, [mismatching indices])."""
+    from oracle import c_oracle
+    distinct = {}
+    for i in got:
+        distinct.setdefault(id(pics[i]), pics[i])
+    keys = list(distinct)
+    ref = c_oracle.decode(params, [distinct[k] for k in keys], threads=threads, with_recon=False)
+    want = {k: sha_planes(r[1]) for k, r in zip(keys, ref)}
+    bad = [i for i, planes in sorted(got.items()) if sha_planes(planes) != want[id(pics[i])]]
+    return len(got), bad
+
+
+def verify(ctxs, groups, a, threads):
+    """After the timed region: every resident batch's error word (p265r_batch_status: a row-kernel
+    dependency give-up in ANY of its runs) and the planes of pictures_to_check() of every batch,
+    against the C oracle.  -> the line's "verified" object."""
+    from p265_amd import _lib
+    n_checked, bad, status_ok, distinct = 0, [], True, set()
+    for (ctx, batches), (params, gp) in zip(ctxs, groups):
+        idx = pictures_to_check(len(gp), a.unique if a.workload == "c3" else len(gp))
+        distinct |= {id(gp[i]) for i in idx}
+        for bi, b in enumerate(batches):
+            try:
+                ctx.status(b)
+            except _lib.P265RError as e:
+                status_ok = False
+                bad.append("batch %d: %s" % (bi, e))
+                continue
+            outs = ctx.download(b, only=idx)
+            n, mism = verify_planes(params, gp, {i: outs[i] for i in idx}, threads)
+            n_checked += n
+            bad += ["batch %d picture %d" % (bi, i) for i in mism]
+    return {"ok": status_ok and not bad, "pictures": n_checked, "distinct": len(distinct),
+            "batches": sum(len(b) for _, b in ctxs), "status_ok": status_ok, "mismatches": bad[:8],
+            "how": "after the timed runs: p265r_batch_status (sticky row-kernel error word) of every resident "
+                   "batch, then the decoded planes of its first and last pictures (SHA-256) against "
+                   "oracle/recon_oracle.c on the same records"}
+
+
+def exit_code(out):
+    """Non-zero when the line's own output check failed (the value is then not a result)."""
+    v = out.get("verified")
+    return 3 if v is not None and not v.get("ok") else 0
 
 
 def end_to_end(device, reps=16, threads=16):
@@ -296,7 +362,8 @@ def main():
     py_base = None
     if world_env == 1 and not a.no_cpu_baseline and a.workload == "c3":
         py_base = cpu_baseline_python(host["cpu_share"])
-    rank, world, local = dist.init(device=int(os.environ.get("LOCAL_RANK", "0")), rccl=world_env > 1)
+    rank, world, local = dist.init(device=int(os.environ.get("LOCAL_RANK", "0")),
+                                   rccl=world_env > 1 and not a.no_rccl)
 
     t0 = time.time()
     groups, (cpu_params, cpu_sample, cpu_what), cfg = build_workload(a, rank, world)
@@ -388,6 +455,15 @@ def main():
                     "kernel), so a unit's latency is the one-batch step time; pipelined steps overlap" % len(pics)}
     if exp:
         out["experiment_env"] = exp
+    if world > 1:
+        out["collectives"] = ("control plane only (--no-rccl)" if a.no_rccl else
+                              "ncclBroadcast of the 32-B params (RCCL); barriers + MAX over the control plane")
+    if not a.no_verify:
+        v = verify(ctxs, groups, a, host["cpu_share"])
+        # every rank checks its own batches; the job is ok only if all are
+        v["ranks_failed"] = int(dist.max_over_ranks(0.0 if v["ok"] else 1.0)) if world > 1 else int(not v["ok"])
+        v["ok"] = v["ok"] and v["ranks_failed"] == 0
+        out["verified"] = v
     if rank == 0:
         out["roofline"]["achievable_copy_gbs"] = hip.copy_bandwidth_gbs(local)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -407,7 +483,11 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.finalize()
+    rc = exit_code(out)
+    if rc:
+        sys.stderr.write("bench.py: output check FAILED: %s\n" % json.dumps(out.get("verified")))
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

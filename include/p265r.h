@@ -158,8 +158,15 @@ void p265r_destroy(p265r_ctx* ctx);
 int  p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p265r_batch** out);
 /* Enqueue reconstruction + SAO of every picture of the batch on the context stream. */
 int  p265r_batch_run(p265r_ctx* ctx, p265r_batch* batch);
-/* Wait for the batch and copy its planes into pics[i].out / pics[i].recon. */
+/* Wait for the batch and copy its planes into pics[i].out / pics[i].recon; returns what
+ * p265r_batch_status returns afterwards. */
 int  p265r_batch_download(p265r_ctx* ctx, p265r_batch* batch, const p265r_picture* pics, int n_pics);
+/* Wait for every run enqueued on the batch's stream and report whether any run of the batch
+ * since its upload failed on the device: P265R_OK, or P265R_EHIP when the intra row pipeline
+ * gave up a (capped) dependency wait -- its output is then incomplete (p265r_last_hip_error
+ * says which).  Lets a caller that re-runs a resident batch (a benchmark) check the work it
+ * timed without downloading it.  No counterpart in the reference (which cannot fail this way). */
+int  p265r_batch_status(p265r_ctx* ctx, p265r_batch* batch);
 int  p265r_batch_free(p265r_ctx* ctx, p265r_batch* batch);
 
 /* Convenience: upload + run (asynchronous) ... */

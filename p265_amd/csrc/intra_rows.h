@@ -193,6 +193,11 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ int clip_pel(int v, int maxv) { return min(max(v, 0), maxv); }
 
+// lane l <- lane l - 1 / lane l + 1 of the whole wave (DPP wave_shr:1 / wave_shl:1; the end lane keeps
+// its own value): a one-lane shift without the LDS crossbar round trip of a ds_bpermute
+__device__ __forceinline__ int wave_from_prev(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ int wave_from_next(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false); }
+
 // sum of v over the 32-lane half of the wave (PAIR) or the whole wave; NR = how many 16-lane
 // rows from the start of each half can hold non-zero values (1, 2 or 4: fewer lane reads)
 template <bool PAIR, int NR = 4>
@@ -520,8 +525,8 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     }
     int v = (w0 & J_NONE) ? 128 : raw;
     if (!PAIR && LOG2 == 3 && ((w0 >> 24) & 3u)) {           // [1 2 1] (8.4.4.2.3), 8x8: never strong
-        const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
-        const int vr = __builtin_amdgcn_ds_bpermute(min(k + 1, 4 * n) << 2, v);
+        // neighbours k -/+ 1 by DPP wave shifts (lane k holds sample k for k <= 4n; no LDS round trip)
+        const int vl = wave_from_prev(v), vr = wave_from_next(v);
         const int f = (vl + 2 * v + vr + 2) >> 2;
         v = (k > 0 && k < 4 * n) ? f : v;                       // the two end samples stay unfiltered
     }
@@ -563,8 +568,7 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
     int v = none ? 128 : raw;
     const int r64 = none ? 128 : __builtin_amdgcn_readfirstlane(raw64);     // reference sample 64 (end, unfiltered)
     if ((w0 >> 24) & 3u) {                                    // [1 2 1] (8.4.4.2.3)
-        const int vl = __builtin_amdgcn_ds_bpermute(max(k - 1, 0) << 2, v);
-        const int vr0 = __builtin_amdgcn_ds_bpermute(min(k + 1, 63) << 2, v);
+        const int vl = wave_from_prev(v), vr0 = wave_from_next(v);   // DPP wave shifts
         const int vr = k == 63 ? r64 : vr0;
         const int f = (vl + 2 * v + vr + 2) >> 2;
         v = k > 0 ? f : v;

@@ -33,6 +33,14 @@
 
 using namespace p265r;
 
+// Experiment knobs (measured-slower or diagnostic variants) are compiled in only with
+// -DP265R_EXPERIMENTS=1 (make variant V=exp FLAGS=-DP265R_EXPERIMENTS=1): P265R_SKIP, P265R_STREAM_PRIO,
+// P265R_PIPE_WAVES, P265R_LEAN=0, P265R_FORK_PREP=2, P265R_ROW_WAVES 4 / 6 / 10 / 16, P265R_DEBUG_SYNC.
+// The product build reads only the knobs the GPU parity matrix sets (tests/test_gpu_parity.py).
+#ifndef P265R_EXPERIMENTS
+#define P265R_EXPERIMENTS 0
+#endif
+
 namespace {
 
 thread_local std::string g_last_hip_error;
@@ -88,21 +96,24 @@ struct p265r_ctx {
     p265r_batch* pending = nullptr;
     std::vector<p265r_picture> pending_pics;
     int schedule = 1;          // 0: one launch per anti-diagonal, 1: CU-local row pipeline
-    int row_waves = 0;         // waves per workgroup of the row pipeline (P265R_ROW_WAVES 4, 6, 8, 10, 12, 16);
-                               // 0 = by run: a batch alone 12 (6 per SIMD, 80 VGPRs: lowest latency),
-                               // overlapping other lanes' batches 8 register-lean (room beside it)
+    int row_waves = 0;         // waves per workgroup of the row pipeline (P265R_ROW_WAVES 8, 12; experiments
+                               // build also 4, 6, 10, 16); 0 = by run: a batch alone 12 (6 per SIMD, 80 VGPRs:
+                               // lowest latency), overlapping other lanes' batches 8 (80 VGPRs: room beside it)
+    unsigned lane_busy = 0;    // lanes with a run enqueued since the API last synchronised them (p265r_sync,
+                               // p265r_batch_download / p265r_batch_status of a batch on the lane): the row
+                               // kernel build of a run follows from the call sequence, not from device timing
     int sao_rows = 1;          // SAO-only batches: 1 16-B strip kernel (CTB 32 / 64; 4-B strip kernel for
                                // CTB 16), 2 4-B strip kernel, 0 loop-filter window kernel (P265R_SAO_ROWS)
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
-    int lean = -1;             // W = 8 row kernel build: 0 unconstrained, 1 register-lean, -1 lean only
-                               // while other lanes have work queued (P265R_LEAN)
+    int lean = 1;              // experiments: W = 8 row kernel build 0 unconstrained (P265R_LEAN=0), 1 register-lean
     int luma_lead = -1;        // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD);
                                // -1 = by run: 8 for a batch alone, 5 beside other lanes' batches (round 3,
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
                                // 45.5/44.9/44.4/44.7 M CTU/s; round 1, W=8: lead 0/1/2/3/5/8/17 ->
                                // 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
     bool stream_prio = false;  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
-    int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (P265R_PIPE_WAVES 4, 6, 8)
+    int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (experiments:
+                               // P265R_PIPE_WAVES 4, 6, 8)
     int num_cus = 256;
     bool debug_sync = false;   // P265R_DEBUG_SYNC=1: synchronise + log after every phase (P265R_DEBUG_DIAG
                                // builds also trace the row kernel's waves and print placement statistics)
@@ -327,24 +338,24 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     return P265R_OK;
 }
 
-// alone: no other lane of the context has work queued, so this batch's kernels have the GPU to
-// themselves (fair CU sharing, the unconstrained W = 8 build); otherwise the register-lean build
+// alone: no other lane of the context has a run enqueued (ctx->lane_busy), so this batch's kernels
+// have the GPU to themselves: W = 12 with fair CU sharing; otherwise W = 8 (80 VGPRs, so the residual /
+// prep / SAO waves of the neighbouring batches fit beside it on every SIMD)
 int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
+#if P265R_EXPERIMENTS
     switch (ctx->row_waves) {
-        case 0:
-            if (alone) return launch_rows_w<12, 6>(ctx, b, st, alone);
-            if (ctx->pipe_waves == 4) return launch_rows_w<4, 1>(ctx, b, st, alone);
-            if (ctx->pipe_waves == 6) return launch_rows_w<6, 1>(ctx, b, st, alone);
-            return launch_rows_w<8, 6>(ctx, b, st, alone);
         case 4: return launch_rows_w<4, 1>(ctx, b, st, alone);
         case 6: return launch_rows_w<6, 1>(ctx, b, st, alone);
         case 10: return launch_rows_w<10, 5>(ctx, b, st, alone);
-        case 12: return launch_rows_w<12, 6>(ctx, b, st, alone);
         case 16: return launch_rows_w<16, 1>(ctx, b, st, alone);
-        default:
-            if (ctx->lean == 1 || (ctx->lean < 0 && !alone)) return launch_rows_w<8, 6>(ctx, b, st, alone);
-            return launch_rows_w<8, 1>(ctx, b, st, alone);
+        default: break;
     }
+    if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 4) return launch_rows_w<4, 1>(ctx, b, st, alone);
+    if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 6) return launch_rows_w<6, 1>(ctx, b, st, alone);
+    if (ctx->lean == 0 && (ctx->row_waves == 8 || (ctx->row_waves == 0 && !alone))) return launch_rows_w<8, 1>(ctx, b, st, alone);
+#endif
+    const int w = ctx->row_waves ? ctx->row_waves : (alone ? 12 : 8);
+    return w == 12 ? launch_rows_w<12, 6>(ctx, b, st, alone) : launch_rows_w<8, 6>(ctx, b, st, alone);
 }
 
 }  // namespace
@@ -409,29 +420,36 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.quad = 3;
     if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 7;
     ctx->n_ctus = g.wc * g.hc;
-    // experiment / test knobs read from the environment (bench.py refuses to run with any set)
-    for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_DEBUG_SYNC", "P265R_SAO_ROWS", "P265R_SKIP",
-                          "P265R_LEAN", "P265R_LUMA_LEAD", "P265R_ROW_WAVES", "P265R_FORK_PREP", "P265R_PIPE_WAVES",
-                          "P265R_STREAM_PRIO"})
+    // test knobs of the GPU parity matrix (bench.py refuses to run with any P265R_* variable set)
+    for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_SAO_ROWS", "P265R_LUMA_LEAD", "P265R_ROW_WAVES",
+                          "P265R_FORK_PREP"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
-    if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
-    if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
-    if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : (std::atoi(v) == 1 ? 1 : -1);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::atoi(v) != 0 ? 1 : 0;
+    if (const char* v = std::getenv("P265R_ROW_WAVES")) {
+        const int w = std::atoi(v);
+        if (w == 8 || w == 12) ctx->row_waves = w;
+#if P265R_EXPERIMENTS
+        if (w == 4 || w == 6 || w == 10 || w == 16) ctx->row_waves = w;
+#endif
+    }
+#if P265R_EXPERIMENTS
+    for (const char* k : {"P265R_DEBUG_SYNC", "P265R_SKIP", "P265R_LEAN", "P265R_PIPE_WAVES", "P265R_STREAM_PRIO"})
+        if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
+    if (const char* v = std::getenv("P265R_DEBUG_SYNC")) ctx->debug_sync = v[0] == '1';
+    if (const char* v = std::getenv("P265R_SKIP")) ctx->skip = std::atoi(v) & 7;
+    if (const char* v = std::getenv("P265R_LEAN")) ctx->lean = std::atoi(v) == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("P265R_PIPE_WAVES")) {
         const int w = std::atoi(v);
         if (w == 4 || w == 6 || w == 8) ctx->pipe_waves = w;
     }
-    if (const char* v = std::getenv("P265R_ROW_WAVES")) {
-        const int w = std::atoi(v);
-        if (w == 4 || w == 6 || w == 8 || w == 10 || w == 12 || w == 16) ctx->row_waves = w;
-    }
+    if (const char* v = std::getenv("P265R_STREAM_PRIO")) ctx->stream_prio = std::atoi(v) != 0;
+#endif
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (const char* v = std::getenv("P265R_STREAM_PRIO")) ctx->stream_prio = std::atoi(v) != 0;
     if (e == hipSuccess) e = lane_stream_create(ctx, &ctx->stream);
     if (e == hipSuccess) ctx->lanes.push_back(ctx->stream);
     if (e == hipSuccess) {
@@ -749,6 +767,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // run are still in place, so the output is unchanged while the skipped phase costs nothing
     const int skip = b->runs > 0 ? ctx->skip : 0;
     ++b->runs;
+    ctx->lane_busy |= 1u << b->lane;
     const bool prep = recon && ctx->schedule == 1 && !(skip & 2);
     hipStream_t ps = s;                              // the prep kernel's stream
     if (prep && ctx->fork_prep) {
@@ -816,17 +835,12 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[1], s));
     // ---- intra wavefront ---------------------------------------------------------------
     if (recon && ctx->schedule == 1) {
-        HIP_TRY(hipMemsetAsync(b->d_err, 0, 256 + kRowCuSlots * 16, s));
-        // does another lane still have work queued (batches overlapping)?  hipErrorNotReady is
-        // "busy"; any other error (e.g. a fault in another lane's kernel) is reported, not cleared
-        bool alone = true;
-        for (size_t i = 0; i < ctx->lanes.size(); ++i) {
-            if ((int)i == b->lane) continue;
-            const hipError_t q = hipStreamQuery(ctx->lanes[i]);
-            if (q == hipErrorNotReady) alone = false;
-            else if (q != hipSuccess) return hip_fail(q, "hipStreamQuery");
-        }
-        (void)hipGetLastError();                    // drop the sticky hipErrorNotReady of the queries
+        // per-CU workgroup slots cleared per run; the error word (d_err[0]) is sticky from upload on,
+        // so p265r_batch_status / p265r_batch_download report a give-up in ANY run of the batch
+        HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16, s));
+        // does another lane have a run enqueued that the API has not synchronised since?  (host
+        // state only, so the build a run gets is a function of the call sequence)
+        const bool alone = (ctx->lane_busy & ~(1u << b->lane)) == 0u;
         int rc = launch_rows(ctx, b, s, alone);
         if (rc) return rc;
         ++tm.intra_launches;
@@ -907,7 +921,15 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
                 HIP_TRY(hipMemcpy2DAsync(pics[i].recon[c], wd[c], b->h_pics[i].rec[c], g.stride[c], wd[c], ht[c],
                                          hipMemcpyDeviceToHost, b->stream));
         }
+    return p265r_batch_status(ctx, b);
+}
+
+int p265r_batch_status(p265r_ctx* ctx, p265r_batch* b) {
+    if (!ctx || !b) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    // the lane is idle now (every run on it, of any batch, has completed)
+    ctx->lane_busy &= ~(1u << b->lane);
     int err = 0;
     HIP_TRY(hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
@@ -967,6 +989,7 @@ int p265r_sync(p265r_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->device));
     for (hipStream_t st : ctx->lanes) HIP_TRY(hipStreamSynchronize(st));
     for (hipStream_t st : ctx->aux) if (st) HIP_TRY(hipStreamSynchronize(st));
+    ctx->lane_busy = 0;
     return P265R_OK;
 }
 
@@ -997,9 +1020,11 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
+        "\"experiments_build\": %d, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
-        ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) alone, pipe_waves while other lanes have work",
+        ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) while no other lane has a run enqueued since the API synchronised "
+                                   "it, else pipe_waves",
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
         ctx->pipeline, ctx->fork_prep, ctx->pipe_waves, hwq_env(), ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG
@@ -1007,6 +1032,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
 #else
         0,
 #endif
+        P265R_EXPERIMENTS,
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;
     if (size > 0) {

@@ -121,8 +121,16 @@ def barrier():
 
 
 def gather_digests(digests):
-    """Every rank's list of (unit id, digest) -> one dict on every rank (control plane)."""
+    """Every rank's list of (unit id, digest) -> one dict on every rank (control plane).
+
+    Contract: unit ids are str or int, digests str (hex), int or a list of str -- the list
+    travels as JSON, so anything else (bytes, tuples) is rejected here rather than silently
+    changed."""
     import json
+    for k, v in digests:
+        ok_v = isinstance(v, (str, int)) or (isinstance(v, list) and all(isinstance(x, str) for x in v))
+        if not isinstance(k, (str, int)) or not ok_v:
+            raise TypeError("gather_digests: unit ids and digests must be str or int, got %r: %r" % (k, v))
     g = _group
     if g is None or g.world == 1:
         return dict(digests)
@@ -151,7 +159,8 @@ def exchange(sends, recvs):
         for src, h in got_heads.items():
             (n,) = struct.unpack_from("<I", h, 0)
             sizes[src] = sum(struct.unpack_from("<qQ", h, 4 + 16 * i)[1] for i in range(n))
-        payloads = g.nccl.exchange({d: b"".join(b for _, b in m) for d, m in by_dst.items()},
+        # zero-byte payloads are skipped on both sides (Rccl.exchange filters them too)
+        payloads = g.nccl.exchange({d: p for d, p in ((d, b"".join(b for _, b in m)) for d, m in by_dst.items()) if p},
                                    {s: n for s, n in sizes.items() if n})
     else:
         got = g.ctrl.alltoall({d: heads[d] + b"".join(b for _, b in m) for d, m in by_dst.items()})

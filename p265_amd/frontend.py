@@ -255,8 +255,12 @@ class ReconHook:
                                getattr(pps, "pps_deblocking_filter_disabled_flag", 0)))
         lf_across = getattr(slice_hdr, "slice_loop_filter_across_slices_enabled_flag",
                             getattr(pps, "pps_loop_filter_across_slices_enabled_flag", 1))
+        # the reference's Ctu carries no tile id: TileId lives in pps.tile_id_rs (pps.py:215-227,
+        # read by image.py:65 for availability); a duck-typed ctu.tile_id is the fallback
+        tids = getattr(pps, "tile_id_rs", None)
+        tile_id = int(tids[ctu.addr_rs]) if tids is not None else int(getattr(ctu, "tile_id", 0))
         self.builder.add_ctu(ctu.addr_rs, slice_addr=getattr(ctu, "slice_addr", 0),
-                             tile_id=int(getattr(ctu, "tile_id", 0)),
+                             tile_id=tile_id,
                              lf_across_slices=bool(lf_across),
                              deblocking=not dbk_off,
                              beta_offset_div2=int(getattr(slice_hdr, "slice_beta_offset_div2",

@@ -107,8 +107,15 @@ class Rccl:
 
     def exchange(self, sends, recv_sizes):
         """Point-to-point: sends {dst: bytes}, recv_sizes {src: nbytes} -> {src: bytes}; one
-        ncclGroupStart/End around every ncclSend / ncclRecv (no ordering deadlock)."""
+        ncclGroupStart/End around every ncclSend / ncclRecv (no ordering deadlock).
+
+        Zero-byte messages are dropped on BOTH sides (an empty payload is neither sent nor
+        received; its source maps to b""): RCCL matches a zero-byte ncclSend like any other, so
+        posting it on one side only would pair it with a later exchange's receive."""
         h = lib()
+        sends = {d: b for d, b in sends.items() if len(b)}
+        empty = {s for s, n in recv_sizes.items() if not n}
+        recv_sizes = {s: n for s, n in recv_sizes.items() if n}
         out_bufs, in_bufs = {}, {}
         try:
             for dst, data in sends.items():
@@ -125,7 +132,9 @@ class Rccl:
                       "ncclRecv")
             check(h.ncclGroupEnd(), "ncclGroupEnd")
             self.stream.synchronize()
-            return {src: in_bufs[src].download(n) for src, n in recv_sizes.items()}
+            out = {src: in_bufs[src].download(n) for src, n in recv_sizes.items()}
+            out.update({src: b"" for src in empty})
+            return out
         finally:
             for b in list(out_bufs.values()) + list(in_bufs.values()):
                 b.free()

@@ -153,18 +153,27 @@ class ReconContext:
     def run(self, batch):
         _lib.check(self.lib.p265r_batch_run(self.handle, batch.handle), "p265r_batch_run")
 
-    def download(self, batch, with_recon=False):
-        outs = self._alloc_planes(len(batch.pics))
-        recs = self._alloc_planes(len(batch.pics)) if with_recon else None
-        arr = (_lib.PictureC * len(batch.pics))()
-        for i in range(len(batch.pics)):
+    def download(self, batch, with_recon=False, only=None):
+        """Planes of the batch's pictures (after its last run).  ``only``: indices of the pictures
+        to copy back (the others are not transferred and come back as None)."""
+        n = len(batch.pics)
+        sel = set(range(n)) if only is None else {int(i) for i in only}
+        outs = [[np.empty(s, np.uint8) for s in plane_shapes(self.params)] if i in sel else None for i in range(n)]
+        recs = ([[np.empty(s, np.uint8) for s in plane_shapes(self.params)] if i in sel else None for i in range(n)]
+                if with_recon else None)
+        arr = (_lib.PictureC * n)()
+        for i in sel:
             for k in range(3):
                 arr[i].out[k] = outs[i][k].ctypes.data
                 if recs is not None:
                     arr[i].recon[k] = recs[i][k].ctypes.data
-        _lib.check(self.lib.p265r_batch_download(self.handle, batch.handle, arr, len(batch.pics)),
-                   "p265r_batch_download")
+        _lib.check(self.lib.p265r_batch_download(self.handle, batch.handle, arr, n), "p265r_batch_download")
         return (outs, recs) if with_recon else outs
+
+    def status(self, batch):
+        """Wait for the batch and raise P265RError if any of its runs failed on the device
+        (p265r_batch_status: the row kernel's sticky error word)."""
+        _lib.check(self.lib.p265r_batch_status(self.handle, batch.handle), "p265r_batch_status")
 
     def sync(self):
         _lib.check(self.lib.p265r_sync(self.handle), "p265r_sync")

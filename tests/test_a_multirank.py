@@ -6,6 +6,9 @@ the rank processes start before this process has touched the GPU).
   shard of tests/golden/synth_4k_tiles.bin and the C5 halo exchange with
   loop_filter_across_tiles_enabled_flag = 1.  The gathered results must equal the C oracle /
   the stream's MD5 SEI.
+* bench.py's multi-rank branch (two rank processes on device 0, control plane only: two RCCL
+  ranks cannot share a device): barrier + MAX over ranks, the whole-job value and the post-run
+  output check of both ranks.
 * A one-rank RCCL communicator (ctypes librccl.so.1, no PyTorch) broadcasts the params POD
   through a hipMalloc'd buffer.  Multi-rank RCCL needs one device per rank: it runs in
   bench.py on an 8-GPU node, not here.
@@ -84,6 +87,44 @@ def test_two_rank_processes_decode_their_shards(tmp_path):
             np.testing.assert_array_equal(got[c], whole[c][y0 >> s:y1 >> s, x0 >> s:x1 >> s], err_msg="tile %d c%d" % (t, c))
 
 
+def test_bench_two_ranks_on_one_device():
+    """bench.py --gpus 2 as torch.distributed.run would start it (RANK / WORLD_SIZE / LOCAL_RANK /
+    MASTER_*), both ranks on device 0 with --no-rccl.  Rank 0 prints exactly one line; value =
+    2 ranks x 512 pictures x 510 CTUs x steps / the MAX over ranks of the timed region."""
+    from ranks import free_port
+    port, ctrl = free_port(), free_port()
+    steps = 3
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P265_CTRL_PORT=str(ctrl))
+        env = {k: v for k, v in env.items() if not k.startswith("P265R_")}
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                                       "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-e2e",
+                                       "--no-rccl"], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((out, err))
+    assert all(p.returncode == 0 for p in procs), "\n".join(o + e for o, e in outs)[-4000:]
+    lines0 = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    lines1 = [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+    assert len(lines0) == 1 and not lines1, outs
+    d = json.loads(lines0[0])
+    assert d["n_gpus"] == 2 and d["steps"] == steps and d["config"]["pictures_per_gpu"] == 512
+    assert d["config"]["ctus_per_picture"] == 510
+    elapsed = d["ms_per_step"] * steps * 1e-3
+    assert abs(d["value"] - 2 * 512 * 510 * steps / elapsed) <= 2e-3 * d["value"]
+    assert d["verified"]["ok"] and d["verified"]["ranks_failed"] == 0 and d["verified"]["pictures"] > 0
+    assert "control plane" in d["collectives"]
+
+
 def test_rccl_world1_broadcast_of_the_params():
     from p265_amd import rccl
     comm = rccl.Rccl(0, 1, 0)
@@ -93,5 +134,8 @@ def test_rccl_world1_broadcast_of_the_params():
         assert comm.broadcast(raw, root=0) == raw
         got = comm.exchange({0: b"halo-bytes"}, {0: 10})          # self send / recv in one group
         assert got == {0: b"halo-bytes"}
+        # a zero-byte payload is skipped on both sides (no unmatched zero-byte ncclSend)
+        assert comm.exchange({0: b""}, {0: 0}) == {0: b""}
+        assert comm.exchange({0: b"x"}, {0: 1}) == {0: b"x"}      # and the next exchange still pairs
     finally:
         comm.close()

@@ -41,27 +41,29 @@ def _check(recon_mod, params, pics, label=""):
     return outs
 
 
-# row pipeline variants: waves per workgroup; P265R_QUAD job merging (bit 0 luma 4x4 quads, bit 1
-# chroma 4x4 quads, bit 2 Cb+Cr 8x8 pairs on the general path instead of the fast one); the
-# register-lean W = 8 build (P265R_LEAN=1), fair CU sharing off (P265R_FAIR=0) and job prep on the
-# batch stream (P265R_FORK_PREP=0); the row queue with
-# the luma chain not leading (P265R_LUMA_LEAD=0) and leading by more rows than a picture has (40)
+# row pipeline variants: the two shipped builds (W = 8 and W = 12 waves per workgroup, both 80 VGPRs);
+# P265R_QUAD job merging (bit 0 luma 4x4 quads, bit 1 chroma 4x4 quads, bit 2 Cb+Cr 8x8 pairs on the
+# general path instead of the fast one); fair CU sharing off (P265R_FAIR=0) with job prep on the
+# batch stream (P265R_FORK_PREP=0); the row queue with the luma chain not leading (P265R_LUMA_LEAD=0)
+# and leading by more rows than a picture has (40).  (W = 4 / 6 / 10 / 16 and the unconstrained W = 8
+# build exist only in the experiments build, p265r.hip P265R_EXPERIMENTS.)
 ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
-                "rows_lean": {"P265R_ROW_WAVES": "8", "P265R_LEAN": "1", "P265R_FAIR": "0", "P265R_FORK_PREP": "0"},
-                "rows10": {"P265R_ROW_WAVES": "10", "P265R_LUMA_LEAD": "0"}, "rows12": {"P265R_ROW_WAVES": "12"},
-                "rows16": {"P265R_ROW_WAVES": "16", "P265R_LUMA_LEAD": "40"},
-                "rows4": {"P265R_ROW_WAVES": "4", "P265R_QUAD": "1"},
+                "rows_nofair": {"P265R_ROW_WAVES": "12", "P265R_FAIR": "0", "P265R_FORK_PREP": "0"},
+                "rows_lead0": {"P265R_ROW_WAVES": "8", "P265R_LUMA_LEAD": "0"},
+                "rows12": {"P265R_ROW_WAVES": "12"},
+                "rows_lead40": {"P265R_ROW_WAVES": "12", "P265R_LUMA_LEAD": "40"},
+                "rows_quad1": {"P265R_ROW_WAVES": "12", "P265R_QUAD": "1"},
                 "rows_noquad": {"P265R_ROW_WAVES": "8", "P265R_QUAD": "4"},
                 "rows_lf": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "0"},
                 "rows_saostrip": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "2"}}
 
 
-@pytest.fixture(params=["rows", "rows_auto", "steps", "rows_lean", "rows10", "rows12", "rows16", "rows4", "rows_noquad", "rows_lf",
-                        "rows_saostrip"])
+@pytest.fixture(params=["rows", "rows_auto", "steps", "rows_nofair", "rows_lead0", "rows12", "rows_lead40", "rows_quad1",
+                        "rows_noquad", "rows_lf", "rows_saostrip"])
 def schedule(request, monkeypatch):
-    """Both intra schedules (CU-local row pipeline with 4..16 waves, the register-lean build,
-    with and without the luma / chroma 4x4 quad jobs and the Cb+Cr 8x8 fast path; per-diagonal
-    launches); SAO-only batches by the streaming SAO kernel or the loop-filter kernel."""
+    """Both intra schedules (CU-local row pipeline, W = 8 and 12, with and without the luma / chroma
+    4x4 quad jobs and the Cb+Cr 8x8 fast path; per-diagonal launches); SAO-only batches by the
+    streaming SAO kernel or the loop-filter kernel."""
     if request.param == "steps":
         monkeypatch.setenv("P265R_SCHEDULE", "steps")
     else:
@@ -211,6 +213,29 @@ def test_pipelined_batches(recon_mod, sync_first):
             ref = O.decode_picture(pd, p.as_oracle_dict())[1]
             for c in range(3):
                 np.testing.assert_array_equal(outs[k][i][c], ref[c], err_msg="set %d pic %d c%d" % (k, i, c))
+
+
+def test_batch_status_and_selective_download(recon_mod):
+    """p265r_batch_status after re-runs of a resident batch (the bench's output check) and a
+    download of a subset of its pictures (the others are not transferred)."""
+    params = R.make_params(pic_width=320, pic_height=192)
+    pics = [synth.make_picture(params, 810 + s, perf=True) for s in range(4)]
+    pd = R.params_dict(params)
+    with recon_mod.ReconContext(params) as ctx:
+        ctx.set_pipeline(2)
+        bs = [ctx.upload(pics), ctx.upload(pics)]
+        for _ in range(3):
+            for b in bs:
+                ctx.run(b)
+        for b in bs:
+            ctx.status(b)
+            outs = ctx.download(b, only=[0, 3])
+            assert outs[1] is None and outs[2] is None
+            for i in (0, 3):
+                ref = O.decode_picture(pd, pics[i].as_oracle_dict())[1]
+                for c in range(3):
+                    np.testing.assert_array_equal(outs[i][c], ref[c])
+            b.free()
 
 
 def test_invalid_records_rejected(recon_mod):

@@ -9,6 +9,7 @@ sanity_frontend.json).  Here the cases sanity.bin lacks: NxN CUs with per-PB mod
 read-back surface get_reconstructed_sample (cu.py:617-632, luma coordinates for every
 component).
 """
+import dataclasses
 import json
 import os
 from types import SimpleNamespace as NS
@@ -159,3 +160,33 @@ def test_live_reference_hook_was_verified():
     assert meta["reconhook_identical"] is True
     _, pics = frontend.pictures_from_frontend_npz(os.path.join(GOLDEN, "sanity_frontend.npz"))
     assert meta["reconhook_tb_records"] == sum(len(p.tbs) for p in pics)
+
+
+def test_hook_takes_tile_ids_from_the_pps():
+    """The reference's Ctu has no tile id (ctu.py sets addr_rs / addr_ts / slice_addr only): TileId
+    is pps.tile_id_rs (pps.py:215-227, read by image.py:65).  A 2x2-tiled picture through the hook
+    must carry those ids, or availability and the loop filters would cross the tile edges."""
+    params = R.make_params(pic_width=128, pic_height=128, ctb_log2_size=6, loop_filter_across_tiles=0)
+    hook = frontend.ReconHook(params)
+    sao = NS(sao_type_idx=[0, 0, 0], sao_offset_abs=[[0] * 4] * 3, sao_offset_sign=[[0] * 4] * 3,
+             sao_band_position=[0, 0, 0], sao_eo_class=[0, 0, 0])
+    sh = NS(slice_sao_luma_flag=0, slice_sao_chroma_flag=0)
+    pps = NS(pps_deblocking_filter_disabled_flag=0, pps_loop_filter_across_slices_enabled_flag=1,
+             pps_beta_offset_div2=0, pps_tc_offset_div2=0, tile_id_rs=[0, 1, 2, 3])
+    rng = np.random.default_rng(11)
+    for rs in range(4):
+        cx, cy = (rs % 2) * 64, (rs // 2) * 64
+        for k in range(4):
+            x, y = cx + (k % 2) * 32, cy + (k // 2) * 32
+            hook.on_decode_leaf(_cu(x, y, 5, 0, {(x, y): int(rng.integers(0, 35))}, 4,
+                                    [_leaf(x, y, 5, 0, [1, 0, 0], [_blk(rng, 32), None, None])]))
+        hook.on_ctu_parsed(NS(addr_rs=rs, slice_addr=0, sao=sao), sh, pps)
+    pic = hook.on_end_of_picture()
+    assert list(pic.ctus["tile_id"]) == [0, 1, 2, 3]
+    R.validate(params, pic)
+    # the ids matter: tiles are independent, so the tiled decode differs from the untiled one
+    untiled = pic.ctus.copy()
+    untiled["tile_id"] = 0
+    (rec_t, _), = c_oracle.decode(params, [pic])
+    (rec_f, _), = c_oracle.decode(params, [dataclasses.replace(pic, ctus=untiled)])
+    assert any((rec_t[c] != rec_f[c]).any() for c in range(3))
