@@ -323,28 +323,29 @@ def build_workload(a, rank, world):
               for f in range(a.c5_frames)]
     mine = dist.unit_shard(a.c5_frames, 4, rank, world)
     parts = {f: tiles.split(p4k, frames[f]) for f in sorted({f for f, _ in mine})}
-    groups = {}
-    for f, t in mine:
-        tp, tpic, _ = parts[f][t]
-        tpic.meta["samples"] = int(tp["pic_width"]) * int(tp["pic_height"]) * 3 // 2
-        groups.setdefault(tp.tobytes(), (tp, []))[1].append(tpic)
-    if not groups:
+    units = [parts[f][t] for f, t in mine]
+    if not units:
         raise RuntimeError("c5: rank %d has no tile unit (more ranks than units)" % rank)
-    groups = list(groups.values())
+    for tp, tpic, _ in units:
+        tpic.meta["samples"] = int(tp["pic_width"]) * int(tp["pic_height"]) * 3 // 2
+    # the uneven tiles (1920 x 1088 top, 1920 x 1072 bottom) as ONE ragged batch: one context of the
+    # largest tile's size, every unit with its own size (p265r_picture.pic_width / pic_height)
+    groups = [(tiles.ragged_params(units), [tpic for _, tpic, _ in units])]
     cols, rows = tiles.tile_grid(p4k, frames[0])
     ctus_all = a.c5_frames * sum((cols[i + 1] - cols[i]) * (rows[j + 1] - rows[j])
                                  for i in range(len(cols) - 1) for j in range(len(rows) - 1))
-    pics = [p for _, g in groups for p in g]
+    pics = groups[0][1]
     params = groups[0][0]
     cfg = {"workload": "C5: 4K all-intra + %sSAO (CTU-row SAO kernel), 2x2 uniform tiles x %d frames = %d tile units "
                        "per step over all ranks, %d on this rank" % ("deblocking + " if a.deblocking else "", a.c5_frames,
                                                                      4 * a.c5_frames, len(pics)),
            "pictures_per_gpu": len(pics), "units_per_step": 4 * a.c5_frames,
            "ctus_per_picture": len(pics[0].ctus),
-           "tiles": sorted({"%dx%d" % (int(tp["pic_width"]), int(tp["pic_height"])) for tp, _ in groups}),
+           "tiles": sorted({"%dx%d" % tuple(p.size) for p in pics}),
            "ctus_all_units": ctus_all,
-           "ctb": 64, "parallelism": "(frame, tile) units -> ranks x%d (dist.unit_shard); one context per tile size" % world}
-    return groups, (params, groups[0][1], "%dx%d tile units of 4K frames" % (int(params["pic_width"]), int(params["pic_height"]))), cfg
+           "ctb": 64, "parallelism": "(frame, tile) units -> ranks x%d (dist.unit_shard); one ragged batch (one launch "
+                                     "per phase) for the uneven tile sizes" % world}
+    return groups, (params, pics, "tile units of 4K frames (%s)" % ", ".join(cfg["tiles"])), cfg
 
 
 def main():
@@ -451,8 +452,11 @@ def main():
     if a.workload == "c5":
         out["unit_latency_ms"] = {
             "one_batch_step": round(acc["total_ms"] / a.steps, 4),
-            "note": "the %d tile units of a rank's step run concurrently (one workgroup per unit in the intra "
-                    "kernel), so a unit's latency is the one-batch step time; pipelined steps overlap" % len(pics)}
+            "intra": round(acc["intra_ms"] / a.steps, 4),
+            "note": "the %d tile units of a rank's step are ONE batch (one launch per phase) and run concurrently "
+                    "(the row kernel gives every unit two workgroups of its own, luma and chroma chains, on "
+                    "different CUs), so the one-batch step time is one unit's latency (the slowest unit's); "
+                    "pipelined steps overlap" % len(pics)}
     if exp:
         out["experiment_env"] = exp
     if world > 1:

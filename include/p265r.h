@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define P265R_ABI_VERSION 1u
+#define P265R_ABI_VERSION 2u   /* 2: per-picture size in p265r_picture */
 
 /* error codes */
 #define P265R_OK            0
@@ -132,6 +132,13 @@ typedef struct p265r_picture {
     void*            recon[3];/* optional in-loop-filter input (reconstruction before deblocking
                                  and SAO), same layout; NULL = skip.  Written by download, or
                                  read by upload with P265R_PIC_RECON_INPUT                     */
+    uint16_t         pic_width;  /* this picture's size in luma samples; 0 = the context's      */
+    uint16_t         pic_height; /* (p265r_params).  A batch may mix sizes up to the context's --
+                                 the uneven tiles of one picture decoded as sub-pictures (the
+                                 reference's column / row widths, pps.py:152-227) run in ONE
+                                 launch.  Multiples of 8; the CTU records (PicSizeInCtbsY),
+                                 planes, nofilter map and TB positions are of this size          */
+    uint32_t         reserved;
 } p265r_picture;
 
 /* Per-phase device time of the last run, from HIP events on the context's stream. */

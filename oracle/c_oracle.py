@@ -26,7 +26,22 @@ def load():
 
 
 def decode(params, pics, threads=0, with_recon=True):
-    """[(recon planes, out planes)] for each picture, computed by the C oracle."""
+    """[(recon planes, out planes)] for each picture, computed by the C oracle.  Pictures with a
+    size of their own (Picture.size, a ragged batch) are decoded with their own parameter set."""
+    groups = {}
+    for i, p in enumerate(pics):
+        pp = R.pic_params(params, p)
+        groups.setdefault(pp.tobytes(), (pp, []))[1].append(i)
+    if len(groups) > 1 or (groups and next(iter(groups.values()))[0] is not params):
+        res = [None] * len(pics)
+        for pp, idx in groups.values():
+            for i, r in zip(idx, _decode(pp, [pics[i] for i in idx], threads, with_recon)):
+                res[i] = r
+        return res
+    return _decode(params, pics, threads, with_recon)
+
+
+def _decode(params, pics, threads, with_recon):
     lib = load()
     pc = Params()
     for name, _ in Params._fields_:

@@ -50,7 +50,8 @@ class Params(ctypes.Structure):
 class PictureC(ctypes.Structure):
     _fields_ = [("ctus", ctypes.c_void_p), ("tbs", ctypes.c_void_p), ("n_tbs", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("coef", ctypes.c_void_p), ("n_coef", ctypes.c_uint64),
-                ("nofilter", ctypes.c_void_p), ("out", ctypes.c_void_p * 3), ("recon", ctypes.c_void_p * 3)]
+                ("nofilter", ctypes.c_void_p), ("out", ctypes.c_void_p * 3), ("recon", ctypes.c_void_p * 3),
+                ("pic_width", ctypes.c_uint16), ("pic_height", ctypes.c_uint16), ("reserved", ctypes.c_uint32)]
 
 
 class Timings(ctypes.Structure):
@@ -60,7 +61,7 @@ class Timings(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
-assert ctypes.sizeof(Params) == 32 and ctypes.sizeof(PictureC) == 96
+assert ctypes.sizeof(Params) == 32 and ctypes.sizeof(PictureC) == 104
 
 # every symbol include/p265r.h declares, with (restype, argtypes)
 _vp = ctypes.c_void_p
@@ -106,7 +107,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.p265r_abi_version() != 1:
+        if lib.p265r_abi_version() != 2:
             raise LibraryNotFound("ABI version mismatch")
         _lib = lib
         return lib

@@ -41,6 +41,8 @@ struct DevPic {                 // per picture, device-resident table
     uint8_t* dbk_map;           // per 8x8 luma block (loopfilter.h), nullptr without deblocking
     int32_t  pool_rel;          // residual pool element index of coefficient pool element 0 (<= 0)
     uint32_t zero_off;          // residual pool element index of a 256-sample zero block
+    uint32_t wh;                // this picture's luma size, width | height << 16 (Geo::ragged batches)
+    uint32_t pad_;
 };
 
 // Batch-uniform layout of the per-picture arrays (p265r.hip batch_upload places them at fixed
@@ -69,7 +71,24 @@ struct Geo {                    // batch-uniform geometry
     int quad;                   // intra_prep_kernel merges 4x4 quads into one job: bit 0 luma, bit 1 chroma;
                                 // bit 2 (A/B only): Cb+Cr 8x8 pairs take the general path
                                 // (P265R_QUAD, default 3)
+    int ragged;                 // some picture of the batch is smaller than w x h (DevPic::wh): kernels
+                                // take that picture's size from pic_geo().  Per-picture arrays keep the
+                                // context-size slots (CTU records, job counts, maps, planes) -- a
+                                // picture's CTU raster and map rows use ITS width in CTUs / 8x8 blocks
 };
+
+// Geometry of one picture of a ragged batch: its own size, CTU grid and map width; strides and the
+// per-picture slot sizes stay the context's (take them from the batch Geo before calling this).
+__device__ __forceinline__ Geo pic_geo(Geo g, uint32_t wh) {
+    g.w = (int)(wh & 0xffffu);
+    g.h = (int)(wh >> 16);
+    g.cw = g.w >> 1;
+    g.ch = g.h >> 1;
+    g.wc = (g.w + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+    g.hc = (g.h + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+    g.nf_w = (g.w + 7) >> 3;
+    return g;
+}
 
 __constant__ int8_t  c_angle[35];
 __constant__ int16_t c_inv_angle[35];
@@ -216,6 +235,10 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
     const int cx = step - 2 * cy;
     if (cy >= g.hc || cx < 0 || cx >= g.wc) return;
     const DevPic P = pics[blockIdx.y];
+    if (g.ragged) {
+        g = pic_geo(g, P.wh);
+        if (cy >= g.hc || cx >= g.wc) return;
+    }
     const int ctb = 1 << g.ctb_log2;
     const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
     const int addr = cy * g.wc + cx;

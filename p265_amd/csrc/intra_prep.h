@@ -197,9 +197,14 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     __shared__ LumaJobLds sj[kMaxCtuLuma];
     __shared__ ChromaJobLds sc[kMaxCtuChroma];
     const DevPic P = pics[blockIdx.z];
-    // CTU records from the batch layout (no wait for the DevPic load: both in flight together)
+    // CTU records from the batch layout (no wait for the DevPic load: both in flight together;
+    // slots of the context size, a ragged batch's smaller pictures use the front of theirs)
     const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.z * g.wc * g.hc;
     const int cx = blockIdx.x, cy = blockIdx.y;
+    if (g.ragged) {
+        g = pic_geo(g, P.wh);
+        if (cx >= g.wc || cy >= g.hc) return;
+    }
     const int addr = cy * g.wc + cx;
     const int lane = threadIdx.x;
     const uint32_t angv = lane < 35 ? c_angw[lane] : 0u;

@@ -854,7 +854,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ resid,
                                                            Geo g, int n_pics, int fs_count, int lead,
                                                            int* __restrict__ err_flag,
-                                                           int* __restrict__ dbg) {
+                                                           int* __restrict__ dbg, int split) {
     // debug trace (P265R_DEBUG_DIAG builds, P265R_DEBUG_SYNC=1): host-mapped words, one per wave
 #if defined(P265R_DEBUG_DIAG) && !defined(P265R_DBG_NOTRACE)
 #define P265R_TRACE(code) do { if (dbg && lane == 0) __hip_atomic_store(dbg + blockIdx.x * W + wave, (code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
@@ -865,7 +865,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     RowCtrl& ctl = *reinterpret_cast<RowCtrl*>(smem);
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int units = 2 * g.hc;                       // row units per picture: (cy, luma), (cy, chroma)
+    // row units per picture: (cy, luma), (cy, chroma); split: two workgroups per picture, workgroup
+    // parity = the component chain it runs (4:2:0 intra never couples them: no cross-workgroup sync)
+    const int units = split ? g.hc : 2 * g.hc;
     const int prog_bytes = (fs_count * units * 4 + 15) & ~15;
     int* prog = reinterpret_cast<int*>(smem + 256);
     WaveLds& L = reinterpret_cast<WaveLds*>(smem + 256 + prog_bytes)[wave];
@@ -896,8 +898,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         for (int i = threadIdx.x; i < 35 * 64; i += 64 * W) atab[35 * 16 + i] = angtab_entry<3>(i >> 6, i & 63);
     __syncthreads();
 
-    const int G = gridDim.x;
-    const int b = blockIdx.x;
+    const int G = split ? (int)(gridDim.x >> 1) : (int)gridDim.x;
+    const int b = split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+    const int split_comp = (int)(blockIdx.x & 1u);
     const int n_my = b < n_pics ? (n_pics - b + G - 1) / G : 0;
     const int rows_total = n_my * units;
     const int ctb = 1 << g.ctb_log2;
@@ -950,7 +953,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         // L0 .. L(d-1), then L(d) C0 L(d+1) C1 ..., then the remaining chroma rows.  Either
         // chain's rows stay in order, so a dequeued row's predecessor is always held by a wave.
         int cy, comp;                                      // comp 0: luma chain, 1: chroma (Cb + Cr)
-        {
+        if (split) {
+            cy = rem; comp = split_comp;
+        } else {
             const int d = min(lead, g.hc);
             if (rem < d) {
                 cy = rem; comp = 0;
@@ -965,6 +970,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         const p265r_ctu* ctus = uniform(gload(&Pp->ctus));
         const IntraJob* jobs = uniform(gload(&Pp->jobs));
         const uint32_t* jcount = uniform(gload(&Pp->jcount));
+        // this picture's CTU grid and plane size (a ragged batch: DevPic::wh); the row queue, progress
+        // words and line buffers keep the context's layout
+        int pwc = g.wc, phc = g.hc, pw = g.w, ph = g.h;
+        if (g.ragged) {
+            const Geo pg = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane(*gptr(&Pp->wh)));
+            pwc = pg.wc; phc = pg.hc; pw = pg.w; ph = pg.h;
+        }
         // picture slot reuse: every row of picture j waits until picture j - fs_count (the
         // slot's previous occupant) has completed all its rows; those rows were dequeued
         // earlier and are held by running waves, so this wait always ends.
@@ -972,6 +984,10 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 return __hip_atomic_load(&ctl.done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen * units;
             })) { failed = true; break; }
         P265R_TRACE(3 | (r << 8));
+        if (cy >= phc) {                                   // a row below this (smaller) picture: nothing to do
+            __hip_atomic_fetch_add(&ctl.done[slot], lane == 0 ? 1 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            continue;
+        }
         unsigned char* line_cur = lines + (size_t)(slot * 2 + (cy & 1)) * line_bytes;
         const unsigned char* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
         int* my_prog = &prog[(slot * g.hc + cy) * 2 + comp];
@@ -985,13 +1001,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         auto hdr_load = [&](int a) {
             return make_uint2(gload(reinterpret_cast<const uint2*>(ctus + a)).x, *gptr(jcount + a));
         };
-        uint2 hdr_n = hdr_load(cy * g.wc);
+        uint2 hdr_n = hdr_load(cy * pwc);
         uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
         bool pre = false;                                  // rec0 / rec1 hold this CTU's first records
-        for (int cx = 0; cx < g.wc; ++cx) {
+        for (int cx = 0; cx < pwc; ++cx) {
             // ---- wait for the row above (2-CTU lag) -------------------------------------
             if (cy > 0) {
-                const int need = min(cx + 2, g.wc);
+                const int need = min(cx + 2, pwc);
                 if (!wait_until([&] {
                         const int v = __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                         return (v & 0xffff0000) == tag && (v & 0xffff) >= need;
@@ -999,12 +1015,12 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             }
             P265R_TRACE(4 | (cx << 8) | (r << 16));
             const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
-            const int addr = cy * g.wc + cx;
+            const int addr = cy * pwc + cx;
             // this CTU's job list (intra_prep_kernel): first job = its first TB index; job counts:
             // luma in bits 0..15, chroma (listed first) in bits 16..31 (intra_prep.h)
             const uint32_t tb_begin = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
             const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
-            if (cx + 1 < g.wc) hdr_n = hdr_load(addr + 1);   // in flight during this CTU
+            if (cx + 1 < pwc) hdr_n = hdr_load(addr + 1);    // in flight during this CTU
             const int n_chroma = (int)(jc >> 16);
             const int nt = comp ? n_chroma : (int)(jc & 0xffffu);
             const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
@@ -1086,6 +1102,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 rn = issue(cur, 0);
             }
             pre = false;
+#ifdef P265R_JOB_UNROLL
+#pragma unroll P265R_JOB_UNROLL
+#endif
             for (int t = 0; t < nt; ++t) {
 #ifdef P265R_JOB_STATS
                 const long long tj0 = __builtin_amdgcn_s_memtime();
@@ -1151,7 +1170,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #endif
             }
 
-            if (cx + 1 < g.wc) {                           // the next CTU's first 64 job records
+            if (cx + 1 < pwc) {                            // the next CTU's first 64 job records
                 const uint32_t tb2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
                 const uint32_t jc2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
                 const int nc2 = (int)(jc2 >> 16);
@@ -1168,7 +1187,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 if ((c == 0) != (comp == 0)) continue;          // this chain's planes only (wave-uniform)
                 const int sub = c ? 1 : 0;
                 const int cs = ctb >> sub;
-                const int Wd = c ? g.cw : g.w, Ht = c ? g.ch : g.h;
+                const int Wd = c ? pw >> 1 : pw, Ht = c ? ph >> 1 : ph;
                 const int xb = x0 >> sub, yb = y0 >> sub;
                 const int wv = min(cs, Wd - xb), hv = min(cs, Ht - yb);
                 const uint8_t* src = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);

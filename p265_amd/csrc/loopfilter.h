@@ -54,6 +54,10 @@ __device__ __forceinline__ int nib4(int v) { return (v ^ 8) - 8; }   // 4-bit tw
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void dbk_map_kernel(const DevPic* __restrict__ pics, Geo g) {
     const DevPic* P = pics + blockIdx.y;
+    if (g.ragged) {                                              // grid: the context's CTU count
+        g = pic_geo(g, P->wh);
+        if ((int)blockIdx.x >= g.wc * g.hc) return;
+    }
     const p265r_ctu me = P->ctus[blockIdx.x];
     const p265r_tb* tbs = P->tbs + me.tb_begin;
     uint8_t* map = P->dbk_map;
@@ -220,10 +224,16 @@ __global__ __launch_bounds__(LfShape<CTBL>::threads(DBK)) void loopfilter_kernel
     const int n_ctus = g.wc * g.hc;
     const int unit = xcd_unit(blockIdx.x, n_ctus * n_pics);
     if (unit >= n_ctus * n_pics) return;                         // whole workgroup: before any barrier
-    const int pic = unit / n_ctus, rs = unit - pic * n_ctus;
+    const int pic = unit / n_ctus;
+    int rs = unit - pic * n_ctus;
     const DevPic* P = pics + pic;
     const p265r_ctu* ctus = P->ctus;
     const int rx = rs % g.wc, ry = rs / g.wc;
+    if (g.ragged) {                                              // this picture's size and CTU raster
+        g = pic_geo(g, P->wh);
+        if (rx >= g.wc || ry >= g.hc) return;                    // whole workgroup: before any barrier
+        rs = ry * g.wc + rx;
+    }
     const int x0 = rx * S, y0 = ry * S, xc0 = x0 >> 1, yc0 = y0 >> 1;
     const int tid = threadIdx.x;
     constexpr int T = SH::threads(DBK);

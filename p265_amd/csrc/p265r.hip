@@ -106,6 +106,8 @@ struct p265r_ctx {
                                // CTB 16), 2 4-B strip kernel, 0 loop-filter window kernel (P265R_SAO_ROWS)
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = 1;              // experiments: W = 8 row kernel build 0 unconstrained (P265R_LEAN=0), 1 register-lean
+    int split = 1;             // component split of small batches (P265R_SPLIT=0: off; launch_rows_w)
+    bool last_split = false;   // the last row-kernel launch was split (p265r_describe)
     int luma_lead = -1;        // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD);
                                // -1 = by run: 8 for a batch alone, 5 beside other lanes' batches (round 3,
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
@@ -155,6 +157,8 @@ struct p265r_batch {
     bool sao = false;
     bool dbk = false;          // some CTU of the batch has deblocking on
     bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
+    bool ragged = false;       // some picture is smaller than the context size (Geo::ragged)
+    std::vector<std::array<int, 2>> size;   // per picture: luma width, height
     int runs = 0;              // p265r_batch_run calls so far
 };
 
@@ -189,15 +193,28 @@ hipError_t lane_stream_create(const p265r_ctx* ctx, hipStream_t* st) {
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
 }
 
+// a picture's luma size: its own (p265r_picture.pic_width / pic_height) or the context's
+std::array<int, 2> pic_size(const p265r_ctx* ctx, const p265r_picture& pic) {
+    return {pic.pic_width ? (int)pic.pic_width : (int)ctx->params.pic_width,
+            pic.pic_height ? (int)pic.pic_height : (int)ctx->params.pic_height};
+}
+
 int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
     const p265r_params& p = ctx->params;
-    const Geo& g = ctx->geo;
+    const auto sz = pic_size(ctx, pic);
+    const int pw = sz[0], ph = sz[1];
+    if (pw > p.pic_width || ph > p.pic_height || pw % 8 || ph % 8 || pw <= 0 || ph <= 0) return P265R_EINVAL;
+    if (pic.reserved) return P265R_EINVAL;
+    Geo g = ctx->geo;
+    g.wc = (pw + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+    g.hc = (ph + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+    const int n_ctus = g.wc * g.hc;
     if (!pic.ctus || (!pic.tbs && pic.n_tbs) || (!pic.coef && pic.n_coef)) return P265R_EINVAL;
     if (pic.flags & ~P265R_PIC_RECON_INPUT) return P265R_EINVAL;
     if ((pic.flags & P265R_PIC_RECON_INPUT) && (!pic.recon[0] || !pic.recon[1] || !pic.recon[2])) return P265R_EINVAL;
     const int ctb = 1 << p.ctb_log2_size;
     const int max_tbs = 3 * (ctb / 4) * (ctb / 4) / 2;                  // all-4x4 luma + 4x4 chroma per 8x8
-    for (int rs = 0; rs < ctx->n_ctus; ++rs) {
+    for (int rs = 0; rs < n_ctus; ++rs) {
         const p265r_ctu& c = pic.ctus[rs];
         if ((uint64_t)c.tb_begin + c.tb_count > pic.n_tbs) return P265R_ERANGE;
         if (c.tb_count > max_tbs) return P265R_EINVAL;                  // more TBs than 4x4 units
@@ -223,7 +240,7 @@ int validate_picture(const p265r_ctx* ctx, const p265r_picture& pic) {
             const int sub = t.c_idx ? 1 : 0;
             const int n = 1 << t.log2_size;
             const int xl = t.x << sub, yl = t.y << sub, nl = n << sub;
-            if (xl + nl > p.pic_width || yl + nl > p.pic_height) return P265R_ERANGE;
+            if (xl + nl > pw || yl + nl > ph) return P265R_ERANGE;
             if (xl < cx0 || yl < cy0 || xl + nl > cx0 + ctb || yl + nl > cy0 + ctb) return P265R_ERANGE;
             if ((t.x & 3) || (t.y & 3) || (t.x & (n - 1)) || (t.y & (n - 1))) return P265R_EINVAL;
             if (t.flags & (P265R_TB_CBF | P265R_TB_PCM)) {
@@ -298,6 +315,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
     auto fn = intra_rows_kernel<W, WPE>;
+    bool split = false;
     {
         // every workgroup resident at once and holding a single picture: one slot is enough
         // (a second picture would only wait for the first), and the smaller LDS footprint can
@@ -306,6 +324,10 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(1)));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc1, fn, 64 * W, lds_of(1)));
         if (pc1 >= 1 && b->n_pics <= pc1 * ctx->num_cus) fs = 1;
+        // component split: a picture's luma chain and its chroma chain on two workgroups of their own
+        // (on different CUs) when all of them fit at once -- the latency regime of a few large
+        // pictures / tile units, where one workgroup's W waves on one CU bound the picture's time
+        split = ctx->split && pc1 >= 1 && 2 * (long long)b->n_pics <= (long long)pc1 * ctx->num_cus;
     }
     const size_t lds = lds_of(fs);
     if (lds > 160 * 1024) return P265R_EUNSUPPORTED;
@@ -313,11 +335,12 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds));
     if (per_cu < 1) return P265R_EUNSUPPORTED;
-    const int grid = std::min(b->n_pics, per_cu * ctx->num_cus);
+    const int grid = split ? 2 * b->n_pics : std::min(b->n_pics, per_cu * ctx->num_cus);
     // fair CU sharing pairs the two workgroups of a CU (rank = arrival order & 1): only valid
     // when exactly two fit per CU and all of them are resident for the whole launch (grid <= 2
     // per CU, no workgroup starts after another ends) -- and only worth it for a batch alone
-    g.fair = g.fair && alone && per_cu == 2;
+    g.fair = g.fair && alone && per_cu == 2 && !split;
+    g.ragged = b->ragged ? 1 : 0;
     int* dbg = nullptr;
 #ifdef P265R_DEBUG_DIAG
     if (ctx->debug_sync) {
@@ -327,7 +350,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     }
 #endif
     const int lead = ctx->luma_lead >= 0 ? ctx->luma_lead : (alone ? 8 : 5);
-    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, lead, b->d_err, dbg);
+    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, lead, b->d_err, dbg, split ? 1 : 0);
+    ctx->last_split = split;
     HIP_TRY(hipGetLastError());
 #ifdef P265R_DEBUG_DIAG
     if (dbg) {
@@ -422,11 +446,12 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     // test knobs of the GPU parity matrix (bench.py refuses to run with any P265R_* variable set)
     for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_SAO_ROWS", "P265R_LUMA_LEAD", "P265R_ROW_WAVES",
-                          "P265R_FORK_PREP"})
+                          "P265R_FORK_PREP", "P265R_SPLIT"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';
     if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::atoi(v) != 0 ? 1 : 0;
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
@@ -503,7 +528,19 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     }
     const bool recon_input = (pics[0].flags & P265R_PIC_RECON_INPUT) != 0;
     const Geo& g = ctx->geo;
-    const int nc = ctx->n_ctus;
+    const int nc = ctx->n_ctus;                  // per-picture slots of the context size
+    // per picture: luma size, CTUs, no-filter map bytes (a ragged batch mixes sizes)
+    std::vector<std::array<int, 2>> psize(n_pics);
+    std::vector<int> pnc(n_pics);
+    std::vector<size_t> pnf(n_pics);
+    bool ragged = false;
+    for (int i = 0; i < n_pics; ++i) {
+        psize[i] = pic_size(ctx, pics[i]);
+        const int wc = (psize[i][0] + (1 << g.ctb_log2) - 1) >> g.ctb_log2, hc = (psize[i][1] + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
+        pnc[i] = wc * hc;
+        pnf[i] = (size_t)((psize[i][0] + 7) / 8) * ((psize[i][1] + 7) / 8);
+        ragged |= psize[i][0] != g.w || psize[i][1] != g.h;
+    }
     // ---- pool sizing per class (per picture, so pictures can be packed in parallel) ----
     std::vector<std::array<size_t, N_POOLS>> cnt_pool(n_pics);
     std::vector<std::array<int, RC_NUM>> cnt_job(n_pics);
@@ -537,7 +574,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const bool sao = ctx->params.sample_adaptive_offset != 0;
     bool dbk = false;
     for (int i = 0; i < n_pics && !dbk; ++i)
-        for (int rs = 0; rs < nc; ++rs)
+        for (int rs = 0; rs < pnc[i]; ++rs)
             if (pics[i].ctus[rs].flags & P265R_CTU_DEBLOCK) { dbk = true; break; }
     const bool lf = sao || dbk;                  // separate output planes
     const size_t plane_bytes[3] = {(size_t)g.stride[0] * g.h, (size_t)g.stride[1] * g.ch, (size_t)g.stride[2] * g.ch};
@@ -621,6 +658,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->sao = sao;
     b->dbk = dbk;
     b->recon_input = recon_input;
+    b->ragged = ragged;
+    b->size = psize;
     unsigned char* dbase = static_cast<unsigned char*>(b->mem);
     b->d_pics = reinterpret_cast<DevPic*>(dbase + o_pics);
     b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
@@ -654,7 +693,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     }
     parallel_for(n_pics, [&](int i) {
         const p265r_picture& pic = pics[i];
-        std::memcpy(h_ctus + (size_t)i * nc, pic.ctus, sizeof(p265r_ctu) * nc);
+        std::memcpy(h_ctus + (size_t)i * nc, pic.ctus, sizeof(p265r_ctu) * pnc[i]);
+        if (pnc[i] < nc) std::memset(h_ctus + (size_t)i * nc + pnc[i], 0, sizeof(p265r_ctu) * (nc - pnc[i]));
         p265r_tb* tb_dst = h_tbs + tb_at[i];
         size_t pool_fill[N_POOLS];
         int job_fill[RC_NUM];
@@ -684,6 +724,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         dp.dbk_map = dbk ? dbase + o_map + nf_bytes * i : nullptr;
         dp.pool_rel = -(int32_t)((o_res - o_pool) / sizeof(int16_t));
         dp.zero_off = (uint32_t)pool_total;
+        dp.wh = (uint32_t)psize[i][0] | (uint32_t)psize[i][1] << 16;
+        dp.pad_ = 0;
         if (lf) {
             unsigned char* o = dbase + o_out + pic_plane_bytes * i;
             dp.out[0] = o;
@@ -693,7 +735,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
             for (int c = 0; c < 3; ++c) dp.out[c] = dp.rec[c];
         }
         if (pic.nofilter) {
-            std::memcpy(host + s_nf + nf_at[i] * nf_bytes, pic.nofilter, nf_bytes);
+            std::memcpy(host + s_nf + nf_at[i] * nf_bytes, pic.nofilter, pnf[i]);   // (slot of the context size)
             dp.nofilter = dbase + o_nf + nf_at[i] * nf_bytes;
         } else {
             dp.nofilter = nullptr;
@@ -733,11 +775,12 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     if (e == hipSuccess) e = hipMemsetAsync(dbase + o_ijobs, 0, o_rec - o_ijobs, st);
     if (e == hipSuccess && n_nf) e = hipMemcpyAsync(dbase + o_nf, host + s_nf, nf_bytes * n_nf, hipMemcpyHostToDevice, st);
     if (e == hipSuccess && recon_input) {
-        const int wd[3] = {g.w, g.cw, g.cw}, ht[3] = {g.h, g.ch, g.ch};
         for (int i = 0; i < n_pics && e == hipSuccess; ++i)
-            for (int c = 0; c < 3 && e == hipSuccess; ++c)
+            for (int c = 0; c < 3 && e == hipSuccess; ++c) {
+                const int wd[3] = {psize[i][0], psize[i][0] / 2, psize[i][0] / 2}, ht[3] = {psize[i][1], psize[i][1] / 2, psize[i][1] / 2};
                 e = hipMemcpy2DAsync(b->h_pics[i].rec[c], g.stride[c], pics[i].recon[c], wd[c], wd[c], ht[c],
                                      hipMemcpyHostToDevice, st);
+            }
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) { int rc = hip_fail(e, "upload"); (void)hipFree(b->mem); delete b; return rc; }
@@ -749,7 +792,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = b->stream;
-    const Geo& g = ctx->geo;
+    Geo g = ctx->geo;
+    g.ragged = b->ragged ? 1 : 0;
     p265r_timings tm{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (ctx->timing) {
@@ -827,7 +871,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], 0));
     if (b->dbk) {
         // deblocking edge / QpY map: depends on the records only
-        dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
+        dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);   // (context-size grid)
         ++tm.residual_launches;
     }
     HIP_TRY(hipGetLastError());
@@ -911,9 +955,11 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
     if (!ctx || !b || !pics || n_pics != b->n_pics) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     const Geo& g = ctx->geo;
-    const int wd[3] = {g.w, g.cw, g.cw}, ht[3] = {g.h, g.ch, g.ch};
     for (int i = 0; i < n_pics; ++i)
         for (int c = 0; c < 3; ++c) {
+            const int sub = c ? 1 : 0;
+            const int wd[3] = {b->size[i][0] >> sub, b->size[i][0] >> sub, b->size[i][0] >> sub};
+            const int ht[3] = {b->size[i][1] >> sub, b->size[i][1] >> sub, b->size[i][1] >> sub};
             if (pics[i].out[c])
                 HIP_TRY(hipMemcpy2DAsync(pics[i].out[c], wd[c], b->h_pics[i].out[c], g.stride[c], wd[c], ht[c],
                                          hipMemcpyDeviceToHost, b->stream));
@@ -1015,12 +1061,12 @@ static const char* hwq_env() {
 int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
     if (!ctx || size < 0 || (size > 0 && !buf)) return P265R_EINVAL;
     const Geo& g = ctx->geo;
-    char tmp[768];
+    char tmp[2048];
     const int n = snprintf(tmp, sizeof(tmp),
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
-        "\"experiments_build\": %d, "
+        "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) while no other lane has a run enqueued since the API synchronised "
@@ -1032,7 +1078,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
 #else
         0,
 #endif
-        P265R_EXPERIMENTS,
+        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0,
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;
     if (size > 0) {

@@ -56,6 +56,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void s
     typedef __attribute__((address_space(1))) uint8_t gu8;
     typedef __attribute__((address_space(1))) uint32_t gu32;
     const DevPic* P = pics + pic;
+    if (g.ragged) {                                               // this picture's size and CTU raster
+        g = pic_geo(g, P->wh);
+        if (cy >= g.hc || sx * kSaoStrip >= (c ? g.cw : g.w)) return;   // whole wave, outside this picture
+    }
     const int sub = c ? 1 : 0;
     const int Ls = g.ctb_log2 - sub, cs = 1 << Ls;
     const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;

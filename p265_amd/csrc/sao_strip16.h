@@ -92,6 +92,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     int c, sx;
     if (u < nsl) { c = 0; sx = u; }
     else { c = 1 + (u - nsl) / nsc; sx = (u - nsl) % nsc; }
+    // CTU records: slots of the context size; a ragged batch's smaller picture uses its own raster
+    const uint32_t* crec = reinterpret_cast<const uint32_t*>(v.ctus0 + (size_t)pic * g.wc * g.hc);
+    if (g.ragged) {
+        g = pic_geo(g, pics[pic].wh);
+        if (cy >= g.hc || sx * kSao16Strip >= (c ? g.cw : g.w)) return;   // whole wave, outside this picture
+    }
     const int sub = c ? 1 : 0;
     const int Ls = L - sub, cs = 1 << Ls;
     const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
@@ -114,7 +120,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     for (int k = 0; k < K + 2; ++k) rowv[k] = row_ld(yb - 1 + k);
 
     // ---- this lane's CTB: SAO parameters, 8.7.3.2 permissions of its 3x3 neighbourhood ----------
-    const uint32_t* crec = reinterpret_cast<const uint32_t*>(v.ctus0 + (size_t)pic * g.wc * g.hc);
     const int rs = cy * g.wc + bx;
     u4v nb[9];
 #pragma unroll

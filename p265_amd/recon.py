@@ -111,6 +111,9 @@ class ReconContext:
         arr = (_lib.PictureC * len(pics))()
         for i, p in enumerate(pics):
             R.check_shapes(self.params, p)      # record contents: validated by p265r_batch_upload
+            pp = R.pic_params(self.params, p)
+            if pp is not self.params:           # a smaller picture of a ragged batch
+                arr[i].pic_width, arr[i].pic_height = int(pp["pic_width"]), int(pp["pic_height"])
             ctus = np.ascontiguousarray(p.ctus, R.CTU_DTYPE)
             tbs = np.ascontiguousarray(p.tbs, R.TB_DTYPE)
             coef = np.ascontiguousarray(p.coef, np.int16)
@@ -133,15 +136,15 @@ class ReconContext:
             if p.recon_input is not None:
                 c.flags = R.PIC_RECON_INPUT
                 planes = [np.ascontiguousarray(p.recon_input[k], np.uint8) for k in range(3)]
-                for k, (pl, shp) in enumerate(zip(planes, plane_shapes(self.params))):
+                for k, (pl, shp) in enumerate(zip(planes, plane_shapes(pp))):
                     if pl.shape != shp:
                         raise R.RecordError("recon_input plane %d has shape %s, expected %s" % (k, pl.shape, shp))
                     c.recon[k] = pl.ctypes.data
                 keep += planes
         return arr, keep
 
-    def _alloc_planes(self, n):
-        return [[np.empty(s, np.uint8) for s in plane_shapes(self.params)] for _ in range(n)]
+    def _alloc_planes(self, pics):
+        return [[np.empty(s, np.uint8) for s in plane_shapes(R.pic_params(self.params, p))] for p in pics]
 
     # ---- batch API --------------------------------------------------------------
     def upload(self, pics):
@@ -158,8 +161,9 @@ class ReconContext:
         to copy back (the others are not transferred and come back as None)."""
         n = len(batch.pics)
         sel = set(range(n)) if only is None else {int(i) for i in only}
-        outs = [[np.empty(s, np.uint8) for s in plane_shapes(self.params)] if i in sel else None for i in range(n)]
-        recs = ([[np.empty(s, np.uint8) for s in plane_shapes(self.params)] if i in sel else None for i in range(n)]
+        shp = [plane_shapes(R.pic_params(self.params, p)) for p in batch.pics]
+        outs = [[np.empty(s, np.uint8) for s in shp[i]] if i in sel else None for i in range(n)]
+        recs = ([[np.empty(s, np.uint8) for s in shp[i]] if i in sel else None for i in range(n)]
                 if with_recon else None)
         arr = (_lib.PictureC * n)()
         for i in sel:
@@ -211,8 +215,8 @@ class ReconContext:
 
     # ---- one-shot API (submit / wait) -------------------------------------------------
     def decode(self, pics, with_recon=False):
-        outs = self._alloc_planes(len(pics))
-        recs = self._alloc_planes(len(pics)) if with_recon and pics[0].recon_input is None else None
+        outs = self._alloc_planes(pics)
+        recs = self._alloc_planes(pics) if with_recon and pics[0].recon_input is None else None
         arr, keep = self._pictures_c(pics, outs, recs)
         _lib.check(self.lib.p265r_submit(self.handle, arr, len(pics)), "p265r_submit")
         _lib.check(self.lib.p265r_wait(self.handle), "p265r_wait")

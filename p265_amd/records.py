@@ -17,7 +17,7 @@ from typing import Optional
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2                 # include/p265r.h P265R_ABI_VERSION (2: per-picture size)
 
 TB_CBF, TB_TSKIP, TB_BYPASS, TB_PCM = 0x01, 0x02, 0x04, 0x08
 PIC_RECON_INPUT = 0x01
@@ -82,6 +82,22 @@ def params_dict(p) -> dict:
     return {k: int(p[k]) for k in PARAM_KEYS}
 
 
+def pic_params(params, pic):
+    """The parameter set one picture of a batch decodes with: the context's ``params``, with the
+    picture's own size when it has one (Picture.size, a ragged batch)."""
+    if pic is None or pic.size is None:
+        return params
+    w, h = (int(v) for v in pic.size)
+    if w == int(params["pic_width"]) and h == int(params["pic_height"]):
+        return params
+    if w > int(params["pic_width"]) or h > int(params["pic_height"]) or w <= 0 or h <= 0 or w % 8 or h % 8:
+        raise RecordError("picture size %dx%d does not fit the context's %dx%d (multiples of 8)"
+                          % (w, h, int(params["pic_width"]), int(params["pic_height"])))
+    kw = params_dict(params)
+    kw.update(pic_width=w, pic_height=h)
+    return make_params(**kw)
+
+
 def ctb_grid(p):
     ctb = 1 << int(p["ctb_log2_size"])
     w, h = int(p["pic_width"]), int(p["pic_height"])
@@ -99,6 +115,9 @@ class Picture:
     # P265R_PIC_RECON_INPUT: the reconstruction [Y, Cb, Cr] (uint8) is given; only the
     # in-loop filters run on it (TB records then serve the deblocking map only)
     recon_input: Optional[list] = None
+    # this picture's luma (width, height) when it is smaller than the batch context's params
+    # (p265r_picture.pic_width / pic_height): the uneven tiles of one picture in one batch
+    size: Optional[tuple] = None
 
     def as_oracle_dict(self):
         return {"ctus": self.ctus, "tbs": self.tbs, "coef": self.coef, "nofilter": self.nofilter}
@@ -116,6 +135,7 @@ class RecordError(ValueError):
 def check_shapes(params, pic: Picture):
     """The checks the C ABI cannot do itself (array dtypes and lengths behind the raw
     pointers); everything inside the records is validated again by p265r_batch_upload."""
+    params = pic_params(params, pic)
     wc, hc = ctb_grid(params)
     if pic.ctus.dtype != CTU_DTYPE or pic.tbs.dtype != TB_DTYPE or pic.coef.dtype != np.int16:
         raise RecordError("record dtypes do not match the ABI")
@@ -132,6 +152,7 @@ def validate(params, pic: Picture):
     The kernels assume every record lies inside its CTU and picture; these checks are
     what keeps a malformed record from faulting the GPU.
     """
+    params = pic_params(params, pic)
     wc, hc = ctb_grid(params)
     if pic.ctus.dtype != CTU_DTYPE or pic.tbs.dtype != TB_DTYPE or pic.coef.dtype != np.int16:
         raise RecordError("record dtypes do not match the ABI")

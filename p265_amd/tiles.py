@@ -76,10 +76,21 @@ def split(params, pic, recon_only=False):
                 nf = np.ascontiguousarray(full[y0 // 8:(y0 + th + 7) // 8, x0 // 8:(x0 + tw + 7) // 8]).reshape(-1)
             tpic = R.Picture(ctus=ctus, tbs=np.concatenate(tbs_parts) if tbs_parts else np.zeros(0, R.TB_DTYPE),
                              coef=np.concatenate(coef_parts).astype(np.int16) if coef_parts else np.zeros(0, np.int16),
-                             nofilter=nf, meta={"tile": (tx, ty), "origin": (x0, y0)})
+                             nofilter=nf, meta={"tile": (tx, ty), "origin": (x0, y0)}, size=(tw, th))
             R.validate(tp, tpic)
             out.append((tp, tpic, (x0, y0)))
     return out
+
+
+def ragged_params(parts):
+    """One context for all tile units of ``split`` (uneven tiles included): the parameter set of
+    the largest tile; every tile picture carries its own size (Picture.size), so the units run
+    as ONE ragged batch -- one launch per phase (p265r_picture.pic_width / pic_height)."""
+    tp0 = parts[0][0]
+    kw = dict(R.params_dict(tp0))
+    kw.update(pic_width=max(int(tp["pic_width"]) for tp, _, _ in parts),
+              pic_height=max(int(tp["pic_height"]) for tp, _, _ in parts))
+    return R.make_params(**kw)
 
 
 def stitch(params, tiles, planes_per_tile):

@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 def test_struct_layouts_match_records():
     assert ctypes.sizeof(_lib.Params) == R.PARAMS_DTYPE.itemsize == 32
     assert R.CTU_DTYPE.itemsize == 32 and R.TB_DTYPE.itemsize == 16
-    assert ctypes.sizeof(_lib.PictureC) == 96
+    assert ctypes.sizeof(_lib.PictureC) == 104
     assert ctypes.sizeof(_lib.Timings) == 48
     # offsets the kernels read (intra_rows.h: tb_from_words / res_addr)
     assert R.TB_DTYPE.fields["coef_off"][1] == 12 and R.TB_DTYPE.fields["flags"][1] == 7
@@ -38,14 +38,14 @@ def test_struct_layouts_match_records():
 
 def test_version_errors_and_no_device_path():
     lib = _lib.load()
-    assert lib.p265r_abi_version() == 1
+    assert lib.p265r_abi_version() == 2
     for code in (0, -1, -2, -3, -4, -5, -6, -7):
         assert lib.p265r_strerror(code)
     n = lib.p265r_device_count()
     assert n >= 0
     if n == 0:                                   # CPU container: create must fail cleanly, not crash
         p = _lib.Params()
-        p.version, p.pic_width, p.pic_height, p.chroma_format_idc = 1, 64, 64, 1
+        p.version, p.pic_width, p.pic_height, p.chroma_format_idc = 2, 64, 64, 1
         p.bit_depth_luma = p.bit_depth_chroma = 8
         p.ctb_log2_size, p.min_tb_log2_size, p.max_tb_log2_size = 6, 2, 5
         h = ctypes.c_void_p()
@@ -58,7 +58,7 @@ def test_invalid_params_rejected_before_device():
     p = _lib.Params()
     h = ctypes.c_void_p()
     assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EINVAL      # version 0
-    p.version, p.pic_width, p.pic_height, p.chroma_format_idc = 1, 64, 64, 1
+    p.version, p.pic_width, p.pic_height, p.chroma_format_idc = 2, 64, 64, 1
     p.bit_depth_luma = p.bit_depth_chroma = 10
     p.ctb_log2_size, p.min_tb_log2_size, p.max_tb_log2_size = 6, 2, 5
     assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EUNSUPPORTED  # 10-bit

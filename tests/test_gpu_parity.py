@@ -45,20 +45,22 @@ def _check(recon_mod, params, pics, label=""):
 # P265R_QUAD job merging (bit 0 luma 4x4 quads, bit 1 chroma 4x4 quads, bit 2 Cb+Cr 8x8 pairs on the
 # general path instead of the fast one); fair CU sharing off (P265R_FAIR=0) with job prep on the
 # batch stream (P265R_FORK_PREP=0); the row queue with the luma chain not leading (P265R_LUMA_LEAD=0)
-# and leading by more rows than a picture has (40).  (W = 4 / 6 / 10 / 16 and the unconstrained W = 8
+# and leading by more rows than a picture has (40); small batches run their luma and chroma chains on
+# two workgroups per picture unless P265R_SPLIT=0 (the large-batch layout, which the bench runs).  (W = 4 / 6 / 10 / 16 and the unconstrained W = 8
 # build exist only in the experiments build, p265r.hip P265R_EXPERIMENTS.)
 ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
-                "rows_nofair": {"P265R_ROW_WAVES": "12", "P265R_FAIR": "0", "P265R_FORK_PREP": "0"},
-                "rows_lead0": {"P265R_ROW_WAVES": "8", "P265R_LUMA_LEAD": "0"},
+                "rows_nosplit": {"P265R_SPLIT": "0"},
+                "rows_nofair": {"P265R_ROW_WAVES": "12", "P265R_FAIR": "0", "P265R_FORK_PREP": "0", "P265R_SPLIT": "0"},
+                "rows_lead0": {"P265R_ROW_WAVES": "8", "P265R_LUMA_LEAD": "0", "P265R_SPLIT": "0"},
                 "rows12": {"P265R_ROW_WAVES": "12"},
-                "rows_lead40": {"P265R_ROW_WAVES": "12", "P265R_LUMA_LEAD": "40"},
+                "rows_lead40": {"P265R_ROW_WAVES": "12", "P265R_LUMA_LEAD": "40", "P265R_SPLIT": "0"},
                 "rows_quad1": {"P265R_ROW_WAVES": "12", "P265R_QUAD": "1"},
                 "rows_noquad": {"P265R_ROW_WAVES": "8", "P265R_QUAD": "4"},
                 "rows_lf": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "0"},
                 "rows_saostrip": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "2"}}
 
 
-@pytest.fixture(params=["rows", "rows_auto", "steps", "rows_nofair", "rows_lead0", "rows12", "rows_lead40", "rows_quad1",
+@pytest.fixture(params=["rows", "rows_auto", "rows_nosplit", "steps", "rows_nofair", "rows_lead0", "rows12", "rows_lead40", "rows_quad1",
                         "rows_noquad", "rows_lf", "rows_saostrip"])
 def schedule(request, monkeypatch):
     """Both intra schedules (CU-local row pipeline, W = 8 and 12, with and without the luma / chroma
@@ -213,6 +215,50 @@ def test_pipelined_batches(recon_mod, sync_first):
             ref = O.decode_picture(pd, p.as_oracle_dict())[1]
             for c in range(3):
                 np.testing.assert_array_equal(outs[k][i][c], ref[c], err_msg="set %d pic %d c%d" % (k, i, c))
+
+
+@pytest.mark.parametrize("ctb_log2,deblocking", [(6, False), (5, False), (4, False), (6, "random"), (5, True)])
+def test_ragged_batch(recon_mod, schedule, ctb_log2, deblocking):
+    """Pictures of different sizes in ONE batch (p265r_picture.pic_width / pic_height, up to the
+    context's size): every one equals the oracle decode at its own size -- CTB 64 / 32 (16-sample
+    strip SAO), CTB 16 (4-sample strip SAO), with deblocking (loop-filter kernel), tiles, slices."""
+    big = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=ctb_log2, loop_filter_across_tiles=0)
+    sizes = [(264, 200), (128, 72), (200, 136), (264, 64), (8 << ctb_log2 >> 3, 200), (96, 200)]
+    pics = []
+    for k, (w, h) in enumerate(sizes):
+        pp = R.pic_params(big, R.Picture(ctus=None, tbs=None, coef=None, size=(w, h)))
+        pic = synth.make_picture(pp, 500 + 7 * k + ctb_log2, perf=bool(k % 2), tiles=(2, 1) if k == 2 else (1, 1),
+                                 n_slices=2 if k == 3 else 1, deblocking=deblocking, bypass_rate=0.03 if k == 5 else 0.0)
+        pic.size = (w, h)
+        pics.append(pic)
+    with recon_mod.ReconContext(big) as ctx:
+        outs, recs = ctx.decode(pics, with_recon=True)
+    for i, (pic, (w, h)) in enumerate(zip(pics, sizes)):
+        pp = R.pic_params(big, pic)
+        assert outs[i][0].shape == (h, w)
+        rec_ref, out_ref = O.decode_picture(R.params_dict(pp), pic.as_oracle_dict())
+        for c in range(3):
+            np.testing.assert_array_equal(recs[i][c], rec_ref[c], err_msg="pic %d %dx%d recon c%d" % (i, w, h, c))
+            np.testing.assert_array_equal(outs[i][c], out_ref[c], err_msg="pic %d %dx%d out c%d" % (i, w, h, c))
+
+
+def test_c5_tiles_of_a_real_stream_in_one_batch(recon_mod):
+    """C5 from bytes: the 2 x 2 uneven tiles (1920 x 1088 top, 1920 x 1072 bottom) of the two 4K
+    pictures of synth_4k_tiles.bin as ONE ragged batch; the stitched pictures reproduce the
+    stream's MD5 picture-hash SEI."""
+    import hashlib
+    from p265_amd import bitstream, tiles
+    pics = bitstream.decode_stream(open(os.path.join(GOLDEN, "synth_4k_tiles.bin"), "rb").read())
+    parts = [tiles.split(p.params, p.picture) for p in pics]
+    units = [u for ps in parts for u in ps]
+    assert sorted({(int(tp["pic_width"]), int(tp["pic_height"])) for tp, _, _ in units}) == [(1920, 1072), (1920, 1088)]
+    with recon_mod.ReconContext(tiles.ragged_params(units)) as ctx:
+        outs = ctx.decode([tpic for _, tpic, _ in units])
+    k = 0
+    for p, ps in zip(pics, parts):
+        full = tiles.stitch(p.params, ps, outs[k:k + len(ps)])
+        k += len(ps)
+        assert [hashlib.md5(np.ascontiguousarray(full[c]).tobytes()).digest() for c in range(3)] == p.hash
 
 
 def test_batch_status_and_selective_download(recon_mod):
