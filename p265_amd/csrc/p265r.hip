@@ -82,6 +82,8 @@ bool params_ok(const p265r_params& p) {
 struct p265r_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t up_stream = nullptr;   // uploads: never queued behind a lane's kernels, so batch k+1
+                                       // uploads while batch k decodes (the host waits for it alone)
     p265r_params params{};
     Geo geo{};
     int n_ctus = 0;
@@ -477,6 +479,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = lane_stream_create(ctx, &ctx->stream);
     if (e == hipSuccess) ctx->lanes.push_back(ctx->stream);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
     if (e == hipSuccess) {
         int8_t ang[35];
         int16_t inv[35];
@@ -511,6 +514,7 @@ void p265r_destroy(p265r_ctx* ctx) {
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
     for (auto& e : ctx->spare) (void)hipEventDestroy(e);
     for (size_t i = 1; i < ctx->lanes.size(); ++i) (void)hipStreamDestroy(ctx->lanes[i]);
+    if (ctx->up_stream) (void)hipStreamDestroy(ctx->up_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
     if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
@@ -765,10 +769,10 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         }
     }
     std::memset(host + o_pool + sizeof(int16_t) * pool_total, 0, o_res - o_pool - sizeof(int16_t) * pool_total);  // pool pad
-    // device image: host-filled ranges copied, everything else of [0, o_rec) zero -- stream
-    // ordered behind any earlier work on the reused allocation, complete before returning
-    // (the staging buffer is refilled by the next upload)
-    hipStream_t st = ctx->stream;
+    // device image: host-filled ranges copied, everything else of [0, o_rec) zero, on the upload
+    // stream (a reused allocation's previous batch completed before p265r_batch_free returned);
+    // complete before returning (the staging buffer is refilled by the next upload)
+    hipStream_t st = ctx->up_stream;
     e = hipMemcpyAsync(dbase, host, o_res, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(dbase + o_res, 0, o_jobs[0] - o_res, st);
     if (e == hipSuccess && jobs_bytes) e = hipMemcpyAsync(dbase + o_jobs[0], host + s_jobs, jobs_bytes, hipMemcpyHostToDevice, st);
@@ -989,11 +993,10 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (ctx->pending == b) ctx->pending = nullptr;
-    hipError_t e = hipSuccess;
-    if (b->stream && b->stream != ctx->stream) e = hipStreamSynchronize(b->stream);   // its lane may still run it
+    // its lane may still run it: the allocation is reused by the next upload (another stream)
+    hipError_t e = b->stream ? hipStreamSynchronize(b->stream) : hipSuccess;
     if (b->mem) {
-        // keep the larger of (cache, this allocation) for the next upload; callers free a batch
-        // only once its work is complete (download/sync), and reuse is ordered on ctx->stream
+        // keep the larger of (cache, this allocation) for the next upload (its runs are complete)
         if (!ctx->cache_mem || b->bytes > ctx->cache_bytes) {
             if (ctx->cache_mem) e = hipFree(ctx->cache_mem);
             ctx->cache_mem = b->mem;

@@ -85,25 +85,46 @@ def _chunks(data, size):
         yield data[i:i + size]
 
 
-def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 64, threads: int = 0,
-                  verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4) -> Iterator[DecodedFrame]:
+class StageTimes(dict):
+    """Wall time per stage of decode_chunks' consumer thread (seconds), plus the parser thread's
+    busy time: a stage breakdown of the end-to-end decoder (tools/e2e_profile.py)."""
+
+    def add(self, k, dt):
+        self[k] = self.get(k, 0.0) + dt
+
+
+def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, threads: int = 0,
+                  verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4, depth: int = 2,
+                  stats: Optional[StageTimes] = None) -> Iterator[DecodedFrame]:
     """Decode a stream given as an iterable of byte chunks; yields frames in output order.
 
-    A GPU batch runs when ``batch`` pictures are pending, when the parameter set changes,
-    or -- if the parser has nothing else ready -- when ``min_batch`` are pending."""
+    A GPU batch is formed when ``batch`` pictures are pending, when the parameter set changes,
+    or -- if the parser has nothing else ready -- when ``min_batch`` are pending.  Up to
+    ``depth`` batches are in flight on separate streams of the context (p265r_set_pipeline):
+    batch k+1 is uploaded while batch k decodes, batch k is downloaded while k+1 decodes, and
+    the picture hashes run on a host thread pool behind both."""
+    import collections
+    import time
+    clock = time.perf_counter
     parser = bitstream.StreamParser(threads=threads)
     q = queue.Queue(maxsize=max(1, prefetch))
     stop = threading.Event()
+    st = stats if stats is not None else StageTimes()
 
     def produce():
         try:
             for ch in chunks:
                 if stop.is_set():
                     return
+                t0 = clock()
                 pics = parser.feed(ch)
+                st.add("parse_thread_busy", clock() - t0)
                 if pics:
                     q.put(pics)
-            q.put(parser.feed(b"", flush=True))
+            t0 = clock()
+            last = parser.feed(b"", flush=True)
+            st.add("parse_thread_busy", clock() - t0)
+            q.put(last)
             q.put(None)
         except BaseException as e:  # noqa: BLE001 -- handed to the consumer
             q.put(e)
@@ -113,14 +134,29 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 64, thr
     contexts = {}
     pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
     outq = OutputQueue()
+    inflight = collections.deque()
     rank = 0
 
-    def run(group):
+    def submit(group):
         key = group[0].params.tobytes()
         ctx = contexts.get(key)
         if ctx is None:
             ctx = contexts[key] = recon.ReconContext(group[0].params, device=device)
-        outs = ctx.decode([d.picture for d in group])
+            ctx.set_pipeline(max(1, min(4, depth)))
+        t0 = clock()
+        b = ctx.upload([d.picture for d in group])          # records -> HBM (upload stream)
+        t1 = clock()
+        ctx.run(b)                                          # enqueued; runs while the host goes on
+        st.add("upload", t1 - t0)
+        st.add("run_enqueue", clock() - t1)
+        inflight.append((ctx, b, group))
+
+    def retire():
+        ctx, b, group = inflight.popleft()
+        t0 = clock()
+        outs = ctx.download(b)                              # waits for the batch, planes -> host
+        st.add("download_wait", clock() - t0)
+        b.free()
         ready = []
         for d, planes in zip(group, outs):
             fr = DecodedFrame(poc=d.poc, output_rank=-1, decode_index=int(d.picture.meta["decode_index"]),
@@ -135,7 +171,9 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 64, thr
         nonlocal rank
         fr, d, futs = item
         if futs is not None:
+            t0 = clock()
             fr.hash_ok = all(f.result() == d.hash[c] for c, f in enumerate(futs))
+            st.add("hash_wait", clock() - t0)
             if verify_hash and not fr.hash_ok:
                 raise HashMismatch("picture %d (POC %d): decoded picture hash SEI mismatch" % (fr.decode_index, fr.poc))
         fr.output_rank = rank
@@ -145,23 +183,32 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 64, thr
     try:
         pending = []
         while True:
+            t0 = clock()
             item = q.get()
+            st.add("wait_parser", clock() - t0)
             if isinstance(item, BaseException):
                 raise item
             end = item is None
             for d in item or []:
                 if pending and (len(pending) >= batch or d.params.tobytes() != pending[0].params.tobytes()):
-                    for it in run(pending):
-                        yield emit(it)
+                    submit(pending)
                     pending = []
+                    while len(inflight) >= depth:
+                        for it in retire():
+                            yield emit(it)
                 pending.append(d)
             # the parser has nothing ready right now: decode what is pending instead of waiting
             if pending and (end or (q.empty() and len(pending) >= min_batch)):
-                for it in run(pending):
-                    yield emit(it)
+                submit(pending)
                 pending = []
+                while len(inflight) >= depth:
+                    for it in retire():
+                        yield emit(it)
             if end:
                 break
+        while inflight:
+            for it in retire():
+                yield emit(it)
         for it in outq.flush():
             yield emit(it)
     finally:
@@ -172,15 +219,17 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 64, thr
             except queue.Empty:
                 pass
         pool.shutdown(wait=True)
+        for ctx, b, _ in inflight:
+            b.free()
         for ctx in contexts.values():
             ctx.close()
 
 
-def decode_bytes(data: bytes, device: int = 0, batch: int = 64, threads: int = 0,
-                 verify_hash: bool = True, chunk: int = 1 << 20) -> List[DecodedFrame]:
+def decode_bytes(data: bytes, device: int = 0, batch: int = 16, threads: int = 0,
+                 verify_hash: bool = True, chunk: int = 1 << 20, **kw) -> List[DecodedFrame]:
     """Decode a whole stream held in memory; returns the output pictures in output order."""
     return list(decode_chunks(_chunks(data, chunk), device=device, batch=batch, threads=threads,
-                              verify_hash=verify_hash))
+                              verify_hash=verify_hash, **kw))
 
 
 def _file_chunks(path, chunk):

@@ -1,31 +1,37 @@
-"""Break down the end-to-end decoder's host/GPU time per stage (run on the GPU box)."""
+"""Stage breakdown of the end-to-end decoder (run on the GPU box): bitstream -> native front-end
+-> upload -> HIP decode -> download -> MD5 check, on tests/golden/synth_1080p_4pic.bin x REPS.
+
+    python tools/e2e_profile.py [reps] > gpurun_out/e2e_profile.txt
+"""
+import json
 import os
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import torch  # noqa: F401,E402
-from p265_amd import bitstream, recon  # noqa: E402
+from p265_amd import bitstream, decoder  # noqa: E402
 
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+threads = min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
 one = open(os.path.join(ROOT, "tests", "golden", "synth_1080p_4pic.bin"), "rb").read()
-data = one * 16
-t = time.perf_counter(); pics = bitstream.decode_stream(data, threads=16); print("parse %.3f s" % (time.perf_counter() - t))
-ctx = recon.ReconContext(pics[0].params)
-ctx.decode([pics[0].picture])
-recs = [p.picture for p in pics]
-for bs in (16, 64):
-    t0 = time.perf_counter()
-    up = run = dl = 0.0
-    for i in range(0, len(recs), bs):
-        a = time.perf_counter(); b = ctx.upload(recs[i:i + bs]); up += time.perf_counter() - a
-        a = time.perf_counter(); ctx.run(b); ctx.sync(); run += time.perf_counter() - a
-        a = time.perf_counter(); outs = ctx.download(b); dl += time.perf_counter() - a
-        b.free()
-    tot = time.perf_counter() - t0
-    print("batch %d: total %.3f s upload %.3f run %.3f download %.3f" % (bs, tot, up, run, dl))
-a = time.perf_counter()
-for o, p in zip(outs, pics):
-    for c in range(3):
-        bitstream.plane_hash(o[c], 0)
-print("md5 of %d pictures %.3f s" % (len(outs), time.perf_counter() - a))
+data = one * reps
+bitstream.decode_stream(one, threads=threads)
+t = time.perf_counter()
+pics = bitstream.decode_stream(data, threads=threads)
+parse_s = time.perf_counter() - t
+n_ctu = sum(len(p.picture.ctus) for p in pics)
+print("stream %d pictures, %d CTUs, %.1f MB, threads %d" % (len(pics), n_ctu, len(data) / 1e6, threads))
+print("parse alone: %.3f s  %.0f CTU/s" % (parse_s, n_ctu / parse_s))
+decoder.decode_bytes(one)                                    # warm: contexts, kernels
+rows = []
+for batch, depth in [(64, 1), (16, 1), (16, 2), (8, 2), (16, 3), (32, 2)]:
+    st = decoder.StageTimes()
+    t = time.perf_counter()
+    frames = decoder.decode_bytes(data, batch=batch, threads=threads, depth=depth, stats=st)
+    dt = time.perf_counter() - t
+    assert len(frames) == len(pics) and all(f.hash_ok for f in frames)
+    row = {"batch": batch, "depth": depth, "e2e_s": round(dt, 4), "e2e_ctu_s": round(n_ctu / dt),
+           **{k: round(v, 4) for k, v in sorted(st.items())}}
+    rows.append(row)
+    print(json.dumps(row))
