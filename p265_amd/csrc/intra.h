@@ -236,7 +236,7 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
     if (cy >= g.hc || cx < 0 || cx >= g.wc) return;
     const DevPic P = pics[blockIdx.y];
     if (g.ragged) {
-        g = pic_geo(g, P.wh);
+        g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P.wh));
         if (cy >= g.hc || cx >= g.wc) return;
     }
     const int ctb = 1 << g.ctb_log2;
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
         const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
         const int xb = x0 >> sub, yb = y0 >> sub;
         const uint8_t* plane = P.rec[c];
-        const int st = g.stride[c];
+        const int st = (c ? g.stride[1] : g.stride[0]);
         uint8_t* top = c ? L.ctop[c - 1] : L.ytop;
         uint8_t* left = c ? L.cleft[c - 1] : L.yleft;
         for (int e = lane; e <= 2 * cs; e += 64) {
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
         const int log2 = tb.log2_size, n = 1 << log2;
         const int cs = ctb >> sub;
         const int xr = tb.x - (x0 >> sub), yr = tb.y - (y0 >> sub);   // CTB-relative, component units
-        const int bd = g.bd[c];
+        const int bd = (c ? g.bd[1] : g.bd[0]);
         const int maxv = (1 << bd) - 1;
         uint8_t* interior = c ? L.c[c - 1] : L.y;
         const int ist = c ? 32 : 64;
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
         const uint8_t* src = c ? L.c[c - 1] : L.y;
         const int ist = c ? 32 : 64;
         uint8_t* plane = P.rec[c];
-        const int st = g.stride[c];
+        const int st = (c ? g.stride[1] : g.stride[0]);
         // 4-byte granules (plane widths are multiples of 4: MinCbSize >= 8)
         const int gpr = wv >> 2;
         for (int e = lane; e < gpr * hv; e += 64) {

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.z * g.wc * g.hc;
     const int cx = blockIdx.x, cy = blockIdx.y;
     if (g.ragged) {
-        g = pic_geo(g, P.wh);
+        g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P.wh));
         if (cx >= g.wc || cy >= g.hc) return;
     }
     const int addr = cy * g.wc + cx;

@@ -34,6 +34,12 @@ namespace p265r {
 #define P265R_SPIN_SLEEP 8
 #endif
 
+// SGPR bases of the job loop (LDS base, angle tables, Cb line) behind opaque s_mov copies per job (1), or
+// left to the compiler (0, A/B)
+#ifndef P265R_OPAQUE_S
+#define P265R_OPAQUE_S 1
+#endif
+
 // intraPredAngle 0 (modes 10 / 26) as plain copies in the fast paths (0 = the generic angular code)
 #ifndef P265R_HV_FAST
 #define P265R_HV_FAST 1
@@ -1125,11 +1131,17 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 int ln;
                 asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
                 uint32_t lbase, tl, tc, tcb, tab;
+#if P265R_OPAQUE_S
                 asm volatile("s_mov_b32 %0, %1" : "=s"(lbase) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&L)));
                 asm volatile("s_mov_b32 %0, %1" : "=s"(tab) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)atab)));
+                asm volatile("s_mov_b32 %0, %1" : "=s"(tcb) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ltop_cb)));
+#else
+                lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)&L);
+                tab = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)atab);
+                tcb = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ltop_cb);
+#endif
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"((uint32_t)(uintptr_t)ltop_l));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tc) : "v"((uint32_t)(uintptr_t)ltop_c));
-                asm volatile("s_mov_b32 %0, %1" : "=s"(tcb) : "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ltop_cb)));
                 WaveLds& LL = *reinterpret_cast<WaveLds*>(lds_ptr(lbase));
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
@@ -1193,7 +1205,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const uint8_t* src = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
                 const int ist = c ? 32 : 64;
                 P265R_GLOBAL uint8_t* plane = gptr_w(uniform(gload(&Pp->rec[c])));
-                const int st = g.stride[c];
+                const int st = (c ? g.stride[1] : g.stride[0]);
                 if (cs >= 16) {
                     // 2^lg 16-sample chunks per CTB row (one ds_read_b128 + one 16-B global store per
                     // lane and chunk).  A chunk that straddles the picture's right edge is stored whole:

@@ -55,7 +55,7 @@ __device__ __forceinline__ int nib4(int v) { return (v ^ 8) - 8; }   // 4-bit tw
 __global__ __launch_bounds__(64) void dbk_map_kernel(const DevPic* __restrict__ pics, Geo g) {
     const DevPic* P = pics + blockIdx.y;
     if (g.ragged) {                                              // grid: the context's CTU count
-        g = pic_geo(g, P->wh);
+        g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
         if ((int)blockIdx.x >= g.wc * g.hc) return;
     }
     const p265r_ctu me = P->ctus[blockIdx.x];
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::threads(DBK)) void loopfilter_kernel
     const p265r_ctu* ctus = P->ctus;
     const int rx = rs % g.wc, ry = rs / g.wc;
     if (g.ragged) {                                              // this picture's size and CTU raster
-        g = pic_geo(g, P->wh);
+        g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
         if (rx >= g.wc || ry >= g.hc) return;                    // whole workgroup: before any barrier
         rs = ry * g.wc + rx;
     }
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::threads(DBK)) void loopfilter_kernel
                     if (!(mq & ebit)) continue;
                     const int offs = edge_offs(xp, yp, xq, yq);
                     if (offs < 0) continue;
-                    const int qpi = (((mq & DBK_QP) + (s_map[bp] & DBK_QP) + 1) >> 1) + g.cqp[c];
+                    const int qpi = (((mq & DBK_QP) + (s_map[bp] & DBK_QP) + 1) >> 1) + (c ? g.cqp[1] : g.cqp[0]);
                     const int tc = c_tc_table[min(max(qpc_table(qpi) + 2 + 2 * nib4(offs >> 4), 0), 53)];
                     const bool nop = s_nf[bp] != 0, noq = s_nf[bq] != 0;
                     uint32_t* w = s_cw(c);
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::threads(DBK)) void loopfilter_kernel
             }
         }
     }
-    uint8_t* dst = P->out[c] + (size_t)Y * g.stride[c] + X;
+    uint8_t* dst = P->out[c] + (size_t)Y * (c ? g.stride[1] : g.stride[0]) + X;
     if (NW == 4) *reinterpret_cast<uint4*>(dst) = make_uint4(res[0], res[1], res[2], res[3]);
     else *reinterpret_cast<uint2*>(dst) = make_uint2(res[0], res[1]);
     }

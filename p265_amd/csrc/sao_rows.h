@@ -57,13 +57,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void s
     typedef __attribute__((address_space(1))) uint32_t gu32;
     const DevPic* P = pics + pic;
     if (g.ragged) {                                               // this picture's size and CTU raster
-        g = pic_geo(g, P->wh);
+        g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
         if (cy >= g.hc || sx * kSaoStrip >= (c ? g.cw : g.w)) return;   // whole wave, outside this picture
     }
     const int sub = c ? 1 : 0;
     const int Ls = g.ctb_log2 - sub, cs = 1 << Ls;
     const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
-    const int st = g.stride[c];
+    const int st = (c ? g.stride[1] : g.stride[0]);
     const gu8* src = (const gu8*)P->rec[c];
     gu8* dst = (gu8*)P->out[c];
     const int X = sx * kSaoStrip + 4 * (lane - 1);

@@ -95,13 +95,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     // CTU records: slots of the context size; a ragged batch's smaller picture uses its own raster
     const uint32_t* crec = reinterpret_cast<const uint32_t*>(v.ctus0 + (size_t)pic * g.wc * g.hc);
     if (g.ragged) {
-        g = pic_geo(g, pics[pic].wh);
+        g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)pics[pic].wh));
         if (cy >= g.hc || sx * kSao16Strip >= (c ? g.cw : g.w)) return;   // whole wave, outside this picture
     }
     const int sub = c ? 1 : 0;
     const int Ls = L - sub, cs = 1 << Ls;
     const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
-    const int st = g.stride[c];
+    const int st = (c ? g.stride[1] : g.stride[0]);
     const uint64_t pofs = (uint64_t)pic * v.pic_bytes + v.plane_off[c];
     const gu8* src = (const gu8*)(v.rec0 + pofs);
     gu8* dst = (gu8*)(v.out0 + pofs);
