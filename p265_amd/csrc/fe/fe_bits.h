@@ -135,6 +135,9 @@ private:
 extern const uint8_t kLpsTable[64][4];      // rangeTabLps (Table 9-46; cabac.py:66-132)
 extern const uint8_t kNextStateMps[64];     // transIdxMps (Table 9-47; cabac.py:134-143)
 extern const uint8_t kNextStateLps[64];     // transIdxLps (cabac.py:145-154)
+// both transitions of a context state word (pStateIdx << 1 | valMps), by "the bin was the LPS":
+// kTransTable[s][0] = MPS transition, [s][1] = LPS transition (incl. the valMps flip at state 0)
+extern const uint8_t kTransTable[128][2];
 
 class Cabac {
 public:
@@ -149,46 +152,54 @@ public:
         value_ |= next_byte();
         bits_needed_ = -8;
     }
+    // Branch-free bin decoding: MPS and LPS outcomes computed together and selected (the
+    // MPS / LPS branch of 9.3.4.3.2 mispredicts about as often as the LPS occurs); one shared
+    // renormalization (an MPS range is >= 128, so it shifts by at most 1, as 9.3.4.3.3 does).
     inline int decision(uint16_t& ctx) {
-        uint32_t state = ctx >> 1, mps = ctx & 1;
-        uint32_t lps = kLpsTable[state][(range_ >> 6) & 3];
-        range_ -= lps;
-        uint32_t scaled = range_ << 7;
-        int bin;
-        if (value_ < scaled) {
-            bin = (int)mps;
-            ctx = (uint16_t)((kNextStateMps[state] << 1) | mps);
-            if (scaled < (256u << 7)) {
-                range_ = scaled >> 6;
-                value_ <<= 1;
-                if (++bits_needed_ == 0) refill();
-            }
-        } else {
-            bin = (int)(1 - mps);
-            value_ -= scaled;
-            int nb = renorm_bits(lps);
-            value_ <<= nb;
-            range_ = lps << nb;
-            if (state == 0) mps = 1 - mps;
-            ctx = (uint16_t)((kNextStateLps[state] << 1) | mps);
-            bits_needed_ += nb;
-            if (bits_needed_ >= 0) {
-                value_ |= (uint32_t)next_byte() << bits_needed_;
-                bits_needed_ -= 8;
-            }
+        const uint32_t s = ctx;
+        const uint32_t lps = kLpsTable[s >> 1][(range_ >> 6) & 3];
+        const uint32_t rmps = range_ - lps;
+        const uint32_t scaled = rmps << 7;
+        const uint32_t is_lps = value_ >= scaled ? 1u : 0u;
+        value_ -= scaled & (0u - is_lps);
+        const uint32_t r = is_lps ? lps : rmps;
+        ctx = kTransTable[s][is_lps];
+        const int nb = renorm_bits(r);
+        range_ = r << nb;
+        value_ <<= nb;
+        bits_needed_ += nb;
+        if (bits_needed_ >= 0) {
+            value_ |= (uint32_t)next_byte() << bits_needed_;
+            bits_needed_ -= 8;
         }
-        return bin;
+        return (int)((s & 1u) ^ is_lps);
     }
     inline int bypass() {
         value_ <<= 1;
         if (++bits_needed_ >= 0) refill();
-        uint32_t scaled = range_ << 7;
-        if (value_ >= scaled) { value_ -= scaled; return 1; }
-        return 0;
+        const uint32_t scaled = range_ << 7;
+        const uint32_t b = value_ >= scaled ? 1u : 0u;
+        value_ -= scaled & (0u - b);
+        return (int)b;
     }
+    // n bypass bins (9.3.4.3.4) at once, up to 8 per step: shifting k bits in and dividing by the
+    // scaled range is the same binary long division the bin-by-bin compare / subtract performs
     inline uint32_t bypass_bits(int n) {
         uint32_t v = 0;
-        for (int i = 0; i < n; ++i) v = (v << 1) | (uint32_t)bypass();
+        while (n > 0) {
+            const int k = n < 8 ? n : 8;
+            value_ <<= k;
+            bits_needed_ += k;
+            if (bits_needed_ >= 0) {
+                value_ |= (uint32_t)next_byte() << bits_needed_;
+                bits_needed_ -= 8;
+            }
+            const uint32_t scaled = range_ << 7;
+            const uint32_t q = value_ / scaled;
+            value_ -= q * scaled;
+            v = (v << k) | q;
+            n -= k;
+        }
         return v;
     }
     inline int terminate() {

@@ -42,6 +42,27 @@ const uint8_t kNextStateLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9
                                    24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
                                    33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
 
+// kTransTable[(pStateIdx << 1) | valMps][bin is the LPS]: kNextStateMps / kNextStateLps folded per state word,
+// with the valMps flip of an LPS at pStateIdx 0 (9.3.4.3.2.2); generated from the two tables above
+const uint8_t kTransTable[128][2] = {
+    {2, 1}, {3, 0}, {4, 0}, {5, 1}, {6, 2}, {7, 3}, {8, 4}, {9, 5},
+    {10, 4}, {11, 5}, {12, 8}, {13, 9}, {14, 8}, {15, 9}, {16, 10}, {17, 11},
+    {18, 12}, {19, 13}, {20, 14}, {21, 15}, {22, 16}, {23, 17}, {24, 18}, {25, 19},
+    {26, 18}, {27, 19}, {28, 22}, {29, 23}, {30, 22}, {31, 23}, {32, 24}, {33, 25},
+    {34, 26}, {35, 27}, {36, 26}, {37, 27}, {38, 30}, {39, 31}, {40, 30}, {41, 31},
+    {42, 32}, {43, 33}, {44, 32}, {45, 33}, {46, 36}, {47, 37}, {48, 36}, {49, 37},
+    {50, 38}, {51, 39}, {52, 38}, {53, 39}, {54, 42}, {55, 43}, {56, 42}, {57, 43},
+    {58, 44}, {59, 45}, {60, 44}, {61, 45}, {62, 46}, {63, 47}, {64, 48}, {65, 49},
+    {66, 48}, {67, 49}, {68, 50}, {69, 51}, {70, 52}, {71, 53}, {72, 52}, {73, 53},
+    {74, 54}, {75, 55}, {76, 54}, {77, 55}, {78, 56}, {79, 57}, {80, 58}, {81, 59},
+    {82, 58}, {83, 59}, {84, 60}, {85, 61}, {86, 60}, {87, 61}, {88, 60}, {89, 61},
+    {90, 62}, {91, 63}, {92, 64}, {93, 65}, {94, 64}, {95, 65}, {96, 66}, {97, 67},
+    {98, 66}, {99, 67}, {100, 66}, {101, 67}, {102, 68}, {103, 69}, {104, 68}, {105, 69},
+    {106, 70}, {107, 71}, {108, 70}, {109, 71}, {110, 70}, {111, 71}, {112, 72}, {113, 73},
+    {114, 72}, {115, 73}, {116, 72}, {117, 73}, {118, 74}, {119, 75}, {120, 74}, {121, 75},
+    {122, 74}, {123, 75}, {124, 76}, {125, 77}, {124, 76}, {125, 77}, {126, 126}, {127, 127},
+};
+
 // Flat context index layout (initType 0 only: I slices).
 enum {
     C_SAO_MERGE = 0, C_SAO_TYPE = 1, C_SPLIT_CU = 2, C_TQ_BYPASS = 5, C_PART_MODE = 6, C_PREV_INTRA = 7,
@@ -103,10 +124,49 @@ struct ScanTables {
             i = 0;
             for (x = 0; x < n; ++x)
                 for (y = 0; y < n; ++y) pos[lg][2][i++] = (uint8_t)(x | (y << 4));   // vertical
+            for (int sc = 0; sc < 3; ++sc)
+                for (int k = 0; k < n * n; ++k) inv[lg][sc][pos[lg][sc][k]] = (uint8_t)k;
         }
     }
+    uint8_t inv[4][3][128];                           // scan index of position x | y << 4
 };
 static const ScanTables kScan;
+
+// sig_coeff_flag context index (9.3.4.2.5, absolute, incl. the component's base) of every
+// position of a 4x4 sub-block, in the sub-block's scan order: [c != 0][log2 - 2][scanIdx]
+// [prevCsbf][first sub-block of the TB][n]
+struct SigCtxTables {
+    uint8_t t[2][4][3][4][2][16];
+    SigCtxTables() : t() {
+        static const uint8_t ctx_idx_map[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+        static const uint8_t pattern[4][16] = {
+            {2, 1, 1, 0, 1, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0},     // prevCsbf 0: by xP + yP ([yP][xP] order)
+            {2, 2, 2, 2, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0},     // 1: by yP
+            {2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0},     // 2: by xP
+            {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2}};
+        for (int c = 0; c < 2; ++c)
+            for (int lg = 2; lg <= 5; ++lg)
+                for (int sc = 0; sc < 3; ++sc)
+                    for (int prev = 0; prev < 4; ++prev)
+                        for (int first = 0; first < 2; ++first)
+                            for (int nn = 0; nn < 16; ++nn) {
+                                const int pos = kScan.pos[2][sc][nn];
+                                const int k = ((pos >> 4) << 2) + (pos & 15);
+                                const int base = 63 + (c ? 27 : 0);          // C_SIG + chroma offset
+                                int v;
+                                if (lg == 2) {
+                                    v = base + ctx_idx_map[k];
+                                } else {
+                                    const int add = c == 0 ? (first ? 0 : 3) + (lg == 3 ? (sc == 0 ? 9 : 15) : 21)
+                                                           : (lg == 3 ? 9 : 12);
+                                    v = base + add + pattern[prev][k];
+                                    if (first && k == 0) v = base;            // DC of the TB: sigCtx 0
+                                }
+                                t[c][lg - 2][sc][prev][first][nn] = (uint8_t)v;
+                            }
+    }
+};
+static const SigCtxTables kSigCtx;
 
 static inline int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 
@@ -134,8 +194,10 @@ public:
         qp_map_.assign((size_t)min_cb_w_ * min_cb_h_, 0);
         ipm_.assign((size_t)w4_ * h4_, 1);
         ctu_tbs_.assign(a.size_ctb, {});
-        // every sample is covered by at most one coded TB (or PCM block) per component
-        out_.coef.reserve((size_t)sps_.width * sps_.height * 3 / 2);
+        // every sample is covered by at most one coded TB (or PCM block) per component: the dense
+        // blocks are carved from one arena sized once (uninitialised; trimmed in finish())
+        out_.coef.resize((size_t)sps_.width * sps_.height * 3 / 2 + 1024);
+        coef_used_ = 0;
         out_.ctus.assign(a.size_ctb, p265r_ctu{});
         for (auto& c : out_.ctus) c.flags = P265R_CTU_LF_ACROSS_SLICES;
         qp_bd_y_ = 6 * (sps_.bit_depth_y - 8);
@@ -213,7 +275,18 @@ public:
         }
     }
 
+    // n zeroed coefficients at the end of the picture's arena
+    int16_t* coef_alloc(size_t n, uint32_t& off) {
+        off = (uint32_t)coef_used_;
+        if (coef_used_ + n > out_.coef.size()) out_.coef.resize(std::max(out_.coef.size() * 2, coef_used_ + n));
+        coef_used_ += n;
+        int16_t* p = out_.coef.data() + off;
+        std::memset(p, 0, n * sizeof(int16_t));
+        return p;
+    }
+
     void finish() {
+        out_.coef.resize(coef_used_);
         for (int rs = 0; rs < a_.size_ctb; ++rs)
             if (ctb_slice_[rs] < 0) bs_fail("picture incomplete: CTB not covered by any slice segment");
         size_t total = 0;
@@ -511,9 +584,8 @@ private:
             int n = 1 << lg;
             int pbd = c ? sps_.pcm_bit_depth_c : sps_.pcm_bit_depth_y;
             int bd = c ? sps_.bit_depth_c : sps_.bit_depth_y;
-            uint32_t off = (uint32_t)out_.coef.size();
-            out_.coef.resize(off + (size_t)n * n);
-            int16_t* dst = out_.coef.data() + off;
+            uint32_t off;
+            int16_t* dst = coef_alloc((size_t)n * n, off);
             for (int k = 0; k < n * n; ++k) dst[k] = (int16_t)(br.u(pbd) << (bd - pbd));
             p265r_tb t{};
             t.x = (uint16_t)(c ? x0 >> 1 : x0);
@@ -606,9 +678,8 @@ private:
     // (tu.py:137-340, 396-665).  Returns the coefficient offset of the dense N x N block.
     uint32_t residual_coding(int log2, int c, int pred_mode, int* tskip_out) {
         int n = 1 << log2;
-        uint32_t off = (uint32_t)out_.coef.size();
-        out_.coef.resize(off + (size_t)n * n, 0);
-        int16_t* blk = out_.coef.data() + off;
+        uint32_t off;
+        int16_t* blk = coef_alloc((size_t)n * n, off);
         int tskip = 0;
         if (pps_.transform_skip && !cu_bypass_ && log2 <= 2) tskip = dec(C_TSKIP + (c ? 1 : 0));
         *tskip_out = tskip;
@@ -642,14 +713,8 @@ private:
         const uint8_t* c_scan = kScan.pos[2][scan];
         int sbw = 1 << lsb;
         // sub-block and in-sub-block scan positions of the last coefficient
-        int last_sb = 0, last_pos = 0;
-        {
-            int sx = last_x >> 2, sy = last_y >> 2, cx = last_x & 3, cy = last_y & 3;
-            for (int i = 0; i < sbw * sbw; ++i)
-                if (sb_scan[i] == (sx | (sy << 4))) { last_sb = i; break; }
-            for (int i = 0; i < 16; ++i)
-                if (c_scan[i] == (cx | (cy << 4))) { last_pos = i; break; }
-        }
+        const int last_sb = kScan.inv[lsb][scan][(last_x >> 2) | ((last_y >> 2) << 4)];
+        const int last_pos = kScan.inv[2][scan][(last_x & 3) | ((last_y & 3) << 4)];
         uint8_t csbf[8][8];
         std::memset(csbf, 0, sizeof(csbf));
         const bool sdh = pps_.sign_data_hiding && !cu_bypass_;
@@ -658,14 +723,8 @@ private:
         // the engine lives in registers for the whole TB (copied back at the end)
         Cabac e = cabac_;
         uint16_t* const cx = ctx_;
-        // sig_coeff_flag context per position of a sub-block (9.3.4.2.5), as absolute indices
-        static const uint8_t ctx_idx_map[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
-        static const uint8_t pattern[4][16] = {
-            {2, 1, 1, 0, 1, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0},     // prevCsbf 0: by xP + yP ([yP][xP] order)
-            {2, 2, 2, 2, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0},     // 1: by yP
-            {2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0},     // 2: by xP
-            {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2}};
-        const int sig_base = C_SIG + (c ? 27 : 0);
+        // sig_coeff_flag contexts per position of a sub-block (9.3.4.2.5), tabulated (kSigCtx)
+        const int cc = c ? 1 : 0;
         for (int i = last_sb; i >= 0; --i) {
             int xs = sb_scan[i] & 15, ys = sb_scan[i] >> 4;
             int infer_dc = 0;
@@ -686,22 +745,13 @@ private:
                 sig_pos[nsig++] = last_pos;
             }
             if (csbf[xs][ys]) {
-                uint8_t sctx[16];
-                if (log2 == 2) {
-                    for (int k = 0; k < 16; ++k) sctx[k] = (uint8_t)(sig_base + ctx_idx_map[k]);
-                } else {
-                    int prev = 0;
-                    if (xs + 1 < sbw) prev |= csbf[xs + 1][ys];
-                    if (ys + 1 < sbw) prev |= csbf[xs][ys + 1] << 1;
-                    int add = c == 0 ? ((xs || ys) ? 3 : 0) + ((log2 == 3) ? (scan == 0 ? 9 : 15) : 21)
-                                     : ((log2 == 3) ? 9 : 12);
-                    for (int k = 0; k < 16; ++k) sctx[k] = (uint8_t)(sig_base + add + pattern[prev][k]);
-                    if (xs == 0 && ys == 0) sctx[0] = (uint8_t)sig_base;   // DC of the TB: sigCtx 0
-                }
+                int prev = 0;
+                if (xs + 1 < sbw) prev |= csbf[xs + 1][ys];
+                if (ys + 1 < sbw) prev |= csbf[xs][ys + 1] << 1;
+                const uint8_t* sctx = kSigCtx.t[cc][log2 - 2][scan][prev][(xs | ys) == 0 ? 1 : 0];
                 for (int nn = start; nn >= 0; --nn) {
-                    int pos = c_scan[nn];
                     if (nn > 0 || !infer_dc) {
-                        if (e.decision(cx[sctx[((pos >> 4) << 2) + (pos & 15)]])) {
+                        if (e.decision(cx[sctx[nn]])) {
                             sig_pos[nsig++] = nn;
                             infer_dc = 0;
                         }
@@ -784,6 +834,7 @@ private:
     std::vector<uint8_t> ipm_;
     std::vector<std::vector<p265r_tb>> ctu_tbs_;
     std::vector<p265r_tb> cu_tbs_;
+    size_t coef_used_ = 0;
     const SliceHeader* hdr_ = nullptr;
     const uint8_t* rbsp_ = nullptr;
     size_t rbsp_size_ = 0;

@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdint>
 #include <memory>
+#include <utility>
 #include <vector>
 
 #include "../../../include/p265r.h"
@@ -9,10 +10,21 @@
 
 namespace p265fe {
 
+// an allocator whose value-less construct() leaves the element uninitialised: resize() of the
+// coefficient arena neither zeroes nor touches its pages (each block is zeroed when carved out)
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = DefaultInitAlloc<U>; };
+    DefaultInitAlloc() = default;
+    template <class U> DefaultInitAlloc(const DefaultInitAlloc<U>&) {}
+    template <class U> void construct(U* p) { ::new (static_cast<void*>(p)) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+
 struct PictureRecords {
     std::vector<p265r_ctu> ctus;      // raster order
     std::vector<p265r_tb> tbs;        // grouped by CTU (raster), decode order inside a CTU
-    std::vector<int16_t> coef;        // decode order
+    std::vector<int16_t, DefaultInitAlloc<int16_t>> coef;   // decode order
     std::vector<uint8_t> nofilter;    // empty = none
     uint32_t n_cus = 0;
 };
