@@ -874,7 +874,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     // row units per picture: (cy, luma), (cy, chroma); split: two workgroups per picture, workgroup
     // parity = the component chain it runs (4:2:0 intra never couples them: no cross-workgroup sync)
     const int units = split ? g.hc : 2 * g.hc;
-    const int prog_bytes = (fs_count * units * 4 + 15) & ~15;
+    // progress words: one per (slot, CTU row, component) in either mode (host: launch_rows_w lds_of)
+    const int prog_bytes = (fs_count * 2 * g.hc * 4 + 15) & ~15;
     int* prog = reinterpret_cast<int*>(smem + 256);
     WaveLds& L = reinterpret_cast<WaveLds*>(smem + 256 + prog_bytes)[wave];
     const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
@@ -898,7 +899,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #ifdef P265R_JOB_STATS
     if (threadIdx.x < 28) ctl.pad[threadIdx.x] = 0;
 #endif
-    for (int i = threadIdx.x; i < fs_count * units; i += 64 * W) prog[i] = -1;
+    for (int i = threadIdx.x; i < fs_count * 2 * g.hc; i += 64 * W) prog[i] = -1;
     for (int i = threadIdx.x; i < 35 * 16; i += 64 * W) atab[i] = angtab_entry<2>(i >> 4, i & 15);
     if (P265R_ANGTAB8)
         for (int i = threadIdx.x; i < 35 * 64; i += 64 * W) atab[35 * 16 + i] = angtab_entry<3>(i >> 6, i & 63);
