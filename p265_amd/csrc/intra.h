@@ -77,6 +77,11 @@ struct Geo {                    // batch-uniform geometry
                                 // picture's CTU raster and map rows use ITS width in CTUs / 8x8 blocks
 };
 
+// ragged-batch support compiled into the kernels (0: A/B only -- a ragged batch then decodes wrongly)
+#ifndef P265R_RAGGED
+#define P265R_RAGGED 1
+#endif
+
 // Geometry of one picture of a ragged batch: its own size, CTU grid and map width; strides and the
 // per-picture slot sizes stay the context's (take them from the batch Geo before calling this).
 __device__ __forceinline__ Geo pic_geo(Geo g, uint32_t wh) {
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
     const int cx = step - 2 * cy;
     if (cy >= g.hc || cx < 0 || cx >= g.wc) return;
     const DevPic P = pics[blockIdx.y];
-    if (g.ragged) {
+    if (P265R_RAGGED && g.ragged) {
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P.wh));
         if (cy >= g.hc || cx >= g.wc) return;
     }

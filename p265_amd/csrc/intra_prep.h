@@ -201,7 +201,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     // slots of the context size, a ragged batch's smaller pictures use the front of theirs)
     const p265r_ctu* ctus = v.ctus0 + (size_t)blockIdx.z * g.wc * g.hc;
     const int cx = blockIdx.x, cy = blockIdx.y;
-    if (g.ragged) {
+    if (P265R_RAGGED && g.ragged) {
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P.wh));
         if (cx >= g.wc || cy >= g.hc) return;
     }

@@ -980,7 +980,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         // this picture's CTU grid and plane size (a ragged batch: DevPic::wh); the row queue, progress
         // words and line buffers keep the context's layout
         int pwc = g.wc, phc = g.hc, pw = g.w, ph = g.h;
-        if (g.ragged) {
+        if (P265R_RAGGED && g.ragged) {
             const Geo pg = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane(*gptr(&Pp->wh)));
             pwc = pg.wc; phc = pg.hc; pw = pg.w; ph = pg.h;
         }

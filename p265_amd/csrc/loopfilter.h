@@ -54,7 +54,7 @@ __device__ __forceinline__ int nib4(int v) { return (v ^ 8) - 8; }   // 4-bit tw
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void dbk_map_kernel(const DevPic* __restrict__ pics, Geo g) {
     const DevPic* P = pics + blockIdx.y;
-    if (g.ragged) {                                              // grid: the context's CTU count
+    if (P265R_RAGGED && g.ragged) {                                              // grid: the context's CTU count
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
         if ((int)blockIdx.x >= g.wc * g.hc) return;
     }
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(LfShape<CTBL>::threads(DBK)) void loopfilter_kernel
     const DevPic* P = pics + pic;
     const p265r_ctu* ctus = P->ctus;
     const int rx = rs % g.wc, ry = rs / g.wc;
-    if (g.ragged) {                                              // this picture's size and CTU raster
+    if (P265R_RAGGED && g.ragged) {                                              // this picture's size and CTU raster
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
         if (rx >= g.wc || ry >= g.hc) return;                    // whole workgroup: before any barrier
         rs = ry * g.wc + rx;

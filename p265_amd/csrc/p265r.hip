@@ -525,10 +525,15 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     if (!ctx || !pics || n_pics <= 0 || !out) return P265R_EINVAL;
     *out = nullptr;
     if (n_pics > 65535) return P265R_ERANGE;                     // pictures index a grid dimension
-    for (int i = 0; i < n_pics; ++i) {
-        int rc = validate_picture(ctx, pics[i]);
-        if (rc) return rc;
-        if ((pics[i].flags ^ pics[0].flags) & P265R_PIC_RECON_INPUT) return P265R_EINVAL;
+    {
+        // every record of every picture is checked (on up to 16 host threads: pictures are
+        // independent); the first failing picture's code is returned
+        std::vector<int> vrc(n_pics, 0);
+        parallel_for(n_pics, [&](int i) { vrc[i] = validate_picture(ctx, pics[i]); });
+        for (int i = 0; i < n_pics; ++i) {
+            if (vrc[i]) return vrc[i];
+            if ((pics[i].flags ^ pics[0].flags) & P265R_PIC_RECON_INPUT) return P265R_EINVAL;
+        }
     }
     const bool recon_input = (pics[0].flags & P265R_PIC_RECON_INPUT) != 0;
     const Geo& g = ctx->geo;
@@ -888,7 +893,10 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16, s));
         // does another lane have a run enqueued that the API has not synchronised since?  (host
         // state only, so the build a run gets is a function of the call sequence)
-        const bool alone = (ctx->lane_busy & ~(1u << b->lane)) == 0u;
+        bool alone = (ctx->lane_busy & ~(1u << b->lane)) == 0u;
+#ifdef P265R_ALONE_PIPE
+        alone = alone && ctx->pipeline == 1;       // A/B: a pipelined context never runs the W = 12 build
+#endif
         int rc = launch_rows(ctx, b, s, alone);
         if (rc) return rc;
         ++tm.intra_launches;

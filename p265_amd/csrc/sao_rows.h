@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void s
     typedef __attribute__((address_space(1))) uint8_t gu8;
     typedef __attribute__((address_space(1))) uint32_t gu32;
     const DevPic* P = pics + pic;
-    if (g.ragged) {                                               // this picture's size and CTU raster
+    if (P265R_RAGGED && g.ragged) {                                               // this picture's size and CTU raster
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
         if (cy >= g.hc || sx * kSaoStrip >= (c ? g.cw : g.w)) return;   // whole wave, outside this picture
     }

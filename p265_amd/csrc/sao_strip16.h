@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     else { c = 1 + (u - nsl) / nsc; sx = (u - nsl) % nsc; }
     // CTU records: slots of the context size; a ragged batch's smaller picture uses its own raster
     const uint32_t* crec = reinterpret_cast<const uint32_t*>(v.ctus0 + (size_t)pic * g.wc * g.hc);
-    if (g.ragged) {
+    if (P265R_RAGGED && g.ragged) {
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)pics[pic].wh));
         if (cy >= g.hc || sx * kSao16Strip >= (c ? g.cw : g.w)) return;   // whole wave, outside this picture
     }
