@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
@@ -59,6 +60,8 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 enum { RC_RAW = RC_NUM, N_POOLS = RC_NUM + 1 };
+
+constexpr size_t kDlHalf = 24u << 20;   // download bounce buffer half (p265r_batch_download)
 
 int tb_class(const p265r_tb& t) {
     if (t.flags & (P265R_TB_BYPASS | P265R_TB_PCM)) return RC_RAW;
@@ -140,6 +143,8 @@ struct p265r_ctx {
     std::vector<hipStream_t> aux;     // aux[i]: lane i's prep stream (created on first use)
     std::vector<hipEvent_t> fork_ev, join_ev;
     std::string describe;             // p265r_describe text
+    unsigned char* dl_stage = nullptr;  // pinned download bounce buffer, 2 x kDlHalf (first download)
+    hipEvent_t dl_ev[2] = {nullptr, nullptr};
 };
 
 struct p265r_batch {
@@ -517,12 +522,23 @@ void p265r_destroy(p265r_ctx* ctx) {
     if (ctx->up_stream) (void)hipStreamDestroy(ctx->up_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
+    if (ctx->dl_stage) (void)hipHostFree(ctx->dl_stage);
+    for (hipEvent_t e : ctx->dl_ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
     delete ctx;
 }
 
 int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p265r_batch** out) {
     if (!ctx || !pics || n_pics <= 0 || !out) return P265R_EINVAL;
+#if P265R_EXPERIMENTS
+    // P265R_UPLOAD_TIMES=1 (experiments build): wall time of the upload's stages on stderr
+    const bool ut = std::getenv("P265R_UPLOAD_TIMES") != nullptr;
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> tp;
+#define P265R_UT(name) do { if (ut) tp.emplace_back(name, std::chrono::steady_clock::now()); } while (0)
+#else
+#define P265R_UT(name) do { } while (0)
+#endif
+    P265R_UT("start");
     *out = nullptr;
     if (n_pics > 65535) return P265R_ERANGE;                     // pictures index a grid dimension
     {
@@ -535,6 +551,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
             if ((pics[i].flags ^ pics[0].flags) & P265R_PIC_RECON_INPUT) return P265R_EINVAL;
         }
     }
+    P265R_UT("validate");
     const bool recon_input = (pics[0].flags & P265R_PIC_RECON_INPUT) != 0;
     const Geo& g = ctx->geo;
     const int nc = ctx->n_ctus;                  // per-picture slots of the context size
@@ -554,15 +571,18 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     std::vector<std::array<size_t, N_POOLS>> cnt_pool(n_pics);
     std::vector<std::array<int, RC_NUM>> cnt_job(n_pics);
     parallel_for(n_pics, [&](int i) {
-        cnt_pool[i].fill(0);
-        cnt_job[i].fill(0);
+        // thread-local counters, stored once (neighbouring pictures' counters share cache lines)
+        std::array<size_t, N_POOLS> cp{};
+        std::array<int, RC_NUM> cj{};
         for (uint32_t t = 0; t < pics[i].n_tbs; ++t) {
             const p265r_tb& tb = pics[i].tbs[t];
             if (!(tb.flags & (P265R_TB_CBF | P265R_TB_PCM))) continue;
             const int cls = tb_class(tb);
-            cnt_pool[i][cls] += (size_t)1 << (2 * tb.log2_size);
-            if (cls < RC_NUM) ++cnt_job[i][cls];
+            cp[cls] += (size_t)1 << (2 * tb.log2_size);
+            if (cls < RC_NUM) ++cj[cls];
         }
+        cnt_pool[i] = cp;
+        cnt_job[i] = cj;
     });
     size_t pool_sz[N_POOLS] = {};
     size_t n_tbs_total = 0;
@@ -614,6 +634,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     const size_t o_rec = off; off += pic_plane_bytes * n_pics;
     const size_t o_out = off; if (lf) off += pic_plane_bytes * n_pics;
     const size_t total = align_up(off, 256);
+    P265R_UT("count+layout");
 
     // ---- host staging: [0, o_res) | jobs [o_jobs[0], o_ijobs) | no-filter maps, compact ---------
     const size_t jobs_bytes = o_ijobs - o_jobs[0];
@@ -677,6 +698,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     for (int c = 0; c < RC_NUM; ++c) { b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]); b->n_jobs[c] = n_jobs[c]; }
     b->h_pics.resize(n_pics);
 
+    P265R_UT("alloc");
     p265r_ctu* h_ctus = reinterpret_cast<p265r_ctu*>(host + o_ctus);
     p265r_tb* h_tbs = reinterpret_cast<p265r_tb*>(host + o_tbs);
     int16_t* h_pool = reinterpret_cast<int16_t*>(host + o_pool);
@@ -750,6 +772,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
             dp.nofilter = nullptr;
         }
     });
+    P265R_UT("pack");
     std::memcpy(host + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
     b->view.rec0 = dbase + o_rec;
     b->view.out0 = lf ? dbase + o_out : dbase + o_rec;
@@ -791,7 +814,18 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
                                      hipMemcpyHostToDevice, st);
             }
     }
+    P265R_UT("enqueue");
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+    P265R_UT("h2d");
+#if P265R_EXPERIMENTS
+    if (ut) {
+        fprintf(stderr, "[p265r] upload %d pictures, %.1f MB staged:", n_pics, (double)(o_res + jobs_bytes) / 1e6);
+        for (size_t i = 1; i < tp.size(); ++i)
+            fprintf(stderr, " %s %.2f ms", tp[i].first, std::chrono::duration<double, std::milli>(tp[i].second - tp[i - 1].second).count());
+        fprintf(stderr, "\n");
+    }
+#endif
+#undef P265R_UT
     if (e != hipSuccess) { int rc = hip_fail(e, "upload"); (void)hipFree(b->mem); delete b; return rc; }
     *out = b;
     return P265R_OK;
@@ -967,18 +1001,69 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
     if (!ctx || !b || !pics || n_pics != b->n_pics) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     const Geo& g = ctx->geo;
+    // planes to copy: (host destination, device source, row pitch, width, height)
+    struct Item { void* dst; const unsigned char* src; int pitch, w, h; size_t bytes; };
+    std::vector<Item> items;
     for (int i = 0; i < n_pics; ++i)
         for (int c = 0; c < 3; ++c) {
             const int sub = c ? 1 : 0;
-            const int wd[3] = {b->size[i][0] >> sub, b->size[i][0] >> sub, b->size[i][0] >> sub};
-            const int ht[3] = {b->size[i][1] >> sub, b->size[i][1] >> sub, b->size[i][1] >> sub};
-            if (pics[i].out[c])
-                HIP_TRY(hipMemcpy2DAsync(pics[i].out[c], wd[c], b->h_pics[i].out[c], g.stride[c], wd[c], ht[c],
-                                         hipMemcpyDeviceToHost, b->stream));
+            const int w = b->size[i][0] >> sub, h = b->size[i][1] >> sub;
+            const int pitch = c ? g.stride[1] : g.stride[0];
+            if (pics[i].out[c]) items.push_back({pics[i].out[c], b->h_pics[i].out[c], pitch, w, h, (size_t)w * h});
             if (pics[i].recon[c] && !b->recon_input)
-                HIP_TRY(hipMemcpy2DAsync(pics[i].recon[c], wd[c], b->h_pics[i].rec[c], g.stride[c], wd[c], ht[c],
-                                         hipMemcpyDeviceToHost, b->stream));
+                items.push_back({pics[i].recon[c], b->h_pics[i].rec[c], pitch, w, h, (size_t)w * h});
         }
+    // D2H through two halves of a pinned bounce buffer (DMA at pinned speed; the copy into the
+    // caller's pageable planes runs on host threads while the next chunk's DMA is in flight)
+    if (!ctx->dl_stage) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&ctx->dl_stage), 2 * kDlHalf, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->dl_stage = nullptr;
+        }
+    }
+    if (!ctx->dl_stage) {                                   // no pinned memory: straight pageable copies
+        for (const Item& it : items)
+            HIP_TRY(hipMemcpy2DAsync(it.dst, it.w, it.src, it.pitch, it.w, it.h, hipMemcpyDeviceToHost, b->stream));
+        return p265r_batch_status(ctx, b);
+    }
+    if (!ctx->dl_ev[0]) {
+        HIP_TRY(hipEventCreateWithFlags(&ctx->dl_ev[0], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ctx->dl_ev[1], hipEventDisableTiming));
+    }
+    // chunks: consecutive items of at most kDlHalf bytes (an item larger than that goes alone, direct)
+    std::vector<std::pair<size_t, size_t>> chunks;          // [first, last) item
+    for (size_t i = 0; i < items.size();) {
+        size_t j = i, bytes = 0;
+        while (j < items.size() && (j == i || bytes + items[j].bytes <= kDlHalf)) bytes += items[j++].bytes;
+        chunks.push_back({i, j});
+        i = j;
+    }
+    auto enqueue = [&](size_t k) -> hipError_t {
+        unsigned char* st = ctx->dl_stage + (k & 1) * kDlHalf;
+        size_t off = 0;
+        for (size_t i = chunks[k].first; i < chunks[k].second; ++i) {
+            const Item& it = items[i];
+            hipError_t e = it.bytes > kDlHalf
+                ? hipMemcpy2DAsync(it.dst, it.w, it.src, it.pitch, it.w, it.h, hipMemcpyDeviceToHost, b->stream)
+                : hipMemcpy2DAsync(st + off, it.w, it.src, it.pitch, it.w, it.h, hipMemcpyDeviceToHost, b->stream);
+            if (e != hipSuccess) return e;
+            off += it.bytes;
+        }
+        return hipEventRecord(ctx->dl_ev[k & 1], b->stream);
+    };
+    if (!chunks.empty()) HIP_TRY(enqueue(0));
+    for (size_t k = 0; k < chunks.size(); ++k) {
+        if (k + 1 < chunks.size()) HIP_TRY(enqueue(k + 1));          // into the other half (its copy-out is done)
+        HIP_TRY(hipEventSynchronize(ctx->dl_ev[k & 1]));
+        const unsigned char* st = ctx->dl_stage + (k & 1) * kDlHalf;
+        const size_t first = chunks[k].first, n = chunks[k].second - first;
+        std::vector<size_t> offs(n);
+        for (size_t i = 0, off = 0; i < n; ++i) { offs[i] = off; off += items[first + i].bytes; }
+        parallel_for((int)n, [&](int i) {
+            const Item& it = items[first + i];
+            if (it.bytes <= kDlHalf) std::memcpy(it.dst, st + offs[i], it.bytes);
+        });
+    }
     return p265r_batch_status(ctx, b);
 }
 
