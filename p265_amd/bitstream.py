@@ -15,6 +15,7 @@ keep those buffers alive.  There is no fallback: a missing library raises
 ``UnsupportedStream``.
 """
 import ctypes
+import hashlib
 import os
 import threading
 from dataclasses import dataclass
@@ -146,7 +147,19 @@ def _view(ptr, n, dtype, owner):
 
 
 def plane_hash(plane, hash_type):
-    """decoded_picture_hash value (D.3.19) of one uint8 plane, as the SEI carries it."""
+    """decoded_picture_hash value (D.3.19) of one uint8 plane, as the SEI carries it.
+
+    MD5 of an 8-bit plane is the MD5 of its samples in raster order (one byte each), which
+    hashlib computes without the GIL and faster than the library's portable MD5; CRC and
+    checksum (and the same MD5, for the tests) come from p265fe_plane_hash."""
+    p = np.ascontiguousarray(plane, np.uint8)
+    if int(hash_type) == HASH_MD5:
+        return hashlib.md5(memoryview(p).cast("B")).digest()
+    return plane_hash_native(p, hash_type)
+
+
+def plane_hash_native(plane, hash_type):
+    """p265fe_plane_hash (the library's D.3.19 implementation for MD5, CRC and checksum)."""
     lib = load()
     p = np.ascontiguousarray(plane, np.uint8)
     out = ctypes.create_string_buffer(16)

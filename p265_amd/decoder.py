@@ -93,16 +93,52 @@ class StageTimes(dict):
         self[k] = self.get(k, 0.0) + dt
 
 
+# Back-end contexts kept warm across decode calls (one per device and parameter set, like a
+# decoder session): a context's first upload pins its staging memory and allocates the batch
+# buffer, which a short stream would otherwise pay on every call.  release_contexts() frees them.
+_CONTEXT_CACHE = {}
+_CONTEXT_LOCK = threading.Lock()
+
+
+def _context(params, device, depth):
+    key = (int(device), params.tobytes(), int(depth))
+    with _CONTEXT_LOCK:
+        ctx = _CONTEXT_CACHE.pop(key, None)          # checked out: one user at a time
+    if ctx is None:
+        ctx = recon.ReconContext(params, device=device)
+        ctx.set_pipeline(max(1, min(4, depth)))
+    return key, ctx
+
+
+def _return_context(key, ctx):
+    with _CONTEXT_LOCK:
+        old = _CONTEXT_CACHE.get(key)
+        if old is None:
+            _CONTEXT_CACHE[key] = ctx
+            return
+    ctx.close()
+
+
+def release_contexts():
+    """Free the back-end contexts decode_chunks keeps between calls."""
+    with _CONTEXT_LOCK:
+        ctxs = list(_CONTEXT_CACHE.values())
+        _CONTEXT_CACHE.clear()
+    for c in ctxs:
+        c.close()
+
+
 def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, threads: int = 0,
                   verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4, depth: int = 2,
-                  stats: Optional[StageTimes] = None) -> Iterator[DecodedFrame]:
+                  stats: Optional[StageTimes] = None, cache_contexts: bool = True) -> Iterator[DecodedFrame]:
     """Decode a stream given as an iterable of byte chunks; yields frames in output order.
 
     A GPU batch is formed when ``batch`` pictures are pending, when the parameter set changes,
     or -- if the parser has nothing else ready -- when ``min_batch`` are pending.  Up to
     ``depth`` batches are in flight on separate streams of the context (p265r_set_pipeline):
     batch k+1 is uploaded while batch k decodes, batch k is downloaded while k+1 decodes, and
-    the picture hashes run on a host thread pool behind both."""
+    the picture hashes run on a host thread pool behind both.  Contexts stay warm between
+    calls (``cache_contexts``; ``release_contexts()`` frees them)."""
     import collections
     import time
     clock = time.perf_counter
@@ -141,8 +177,12 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, thr
         key = group[0].params.tobytes()
         ctx = contexts.get(key)
         if ctx is None:
-            ctx = contexts[key] = recon.ReconContext(group[0].params, device=device)
-            ctx.set_pipeline(max(1, min(4, depth)))
+            t0 = clock()
+            ck, ctx = _context(group[0].params, device, depth)
+            contexts[key] = (ck, ctx)
+            st.add("context", clock() - t0)
+        else:
+            ctx = ctx[1]
         t0 = clock()
         b = ctx.upload([d.picture for d in group])          # records -> HBM (upload stream)
         t1 = clock()
@@ -221,8 +261,13 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, thr
         pool.shutdown(wait=True)
         for ctx, b, _ in inflight:
             b.free()
-        for ctx in contexts.values():
-            ctx.close()
+        t0 = clock()
+        for ck, ctx in contexts.values():
+            if cache_contexts:
+                _return_context(ck, ctx)
+            else:
+                ctx.close()
+        st.add("context", clock() - t0)
 
 
 def decode_bytes(data: bytes, device: int = 0, batch: int = 16, threads: int = 0,
