@@ -96,25 +96,26 @@ class StageTimes(dict):
 # Back-end contexts kept warm across decode calls (one per device and parameter set, like a
 # decoder session): a context's first upload pins its staging memory and allocates the batch
 # buffer, which a short stream would otherwise pay on every call.  release_contexts() frees them.
-_CONTEXT_CACHE = {}
+_CONTEXT_CACHE = {}                    # key -> [idle ReconContext]
 _CONTEXT_LOCK = threading.Lock()
 
 
-def _context(params, device, depth):
-    key = (int(device), params.tobytes(), int(depth))
+def _context(params, device, pipeline):
+    key = (int(device), params.tobytes(), int(pipeline))
     with _CONTEXT_LOCK:
-        ctx = _CONTEXT_CACHE.pop(key, None)          # checked out: one user at a time
+        idle = _CONTEXT_CACHE.get(key)
+        ctx = idle.pop() if idle else None         # checked out: one user at a time
     if ctx is None:
         ctx = recon.ReconContext(params, device=device)
-        ctx.set_pipeline(max(1, min(4, depth)))
+        ctx.set_pipeline(max(1, min(4, pipeline)))
     return key, ctx
 
 
-def _return_context(key, ctx):
+def _return_context(key, ctx, keep=8):
     with _CONTEXT_LOCK:
-        old = _CONTEXT_CACHE.get(key)
-        if old is None:
-            _CONTEXT_CACHE[key] = ctx
+        idle = _CONTEXT_CACHE.setdefault(key, [])
+        if len(idle) < keep:
+            idle.append(ctx)
             return
     ctx.close()
 
@@ -122,35 +123,48 @@ def _return_context(key, ctx):
 def release_contexts():
     """Free the back-end contexts decode_chunks keeps between calls."""
     with _CONTEXT_LOCK:
-        ctxs = list(_CONTEXT_CACHE.values())
+        ctxs = [c for idle in _CONTEXT_CACHE.values() for c in idle]
         _CONTEXT_CACHE.clear()
     for c in ctxs:
         c.close()
 
 
-def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, threads: int = 0,
+class _Lane:
+    """One back-end context of the decoder and the lock that serialises its calls: the submit
+    thread uploads into it while the consumer downloads from another one (contexts are not
+    thread-safe, distinct contexts are independent)."""
+
+    def __init__(self, key, ctx):
+        self.key, self.ctx, self.lock = key, ctx, threading.Lock()
+
+
+def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 8, threads: int = 0,
                   verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4, depth: int = 2,
                   stats: Optional[StageTimes] = None, cache_contexts: bool = True) -> Iterator[DecodedFrame]:
     """Decode a stream given as an iterable of byte chunks; yields frames in output order.
 
-    A GPU batch is formed when ``batch`` pictures are pending, when the parameter set changes,
-    or -- if the parser has nothing else ready -- when ``min_batch`` are pending.  Up to
-    ``depth`` batches are in flight on separate streams of the context (p265r_set_pipeline):
-    batch k+1 is uploaded while batch k decodes, batch k is downloaded while k+1 decodes, and
-    the picture hashes run on a host thread pool behind both.  Contexts stay warm between
-    calls (``cache_contexts``; ``release_contexts()`` frees them)."""
-    import collections
+    Three stages run concurrently: the parse thread (native front-end on its own host threads),
+    the submit thread (groups pictures into GPU batches -- ``batch`` pictures, a parameter-set
+    change, or ``min_batch`` when the parser has nothing else ready -- and uploads + enqueues
+    them) and the caller's thread (downloads, checks the picture hashes on a host pool, emits in
+    output order).  Batches alternate over ``depth`` back-end contexts, so batch k+1 uploads
+    while batch k is downloaded; at most ``depth`` batches are in flight.  Contexts stay warm
+    between calls (``cache_contexts``; ``release_contexts()`` frees them)."""
     import time
     clock = time.perf_counter
     parser = bitstream.StreamParser(threads=threads)
     q = queue.Queue(maxsize=max(1, prefetch))
+    done_q = queue.Queue()
+    slots = threading.Semaphore(max(1, depth))
     stop = threading.Event()
     st = stats if stats is not None else StageTimes()
+    depth = max(1, min(4, depth))
 
     def produce():
         try:
             for ch in chunks:
                 if stop.is_set():
+                    q.put(None)         # the submitter ends on it (the consumer drains q)
                     return
                 t0 = clock()
                 pics = parser.feed(ch)
@@ -165,38 +179,74 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, thr
         except BaseException as e:  # noqa: BLE001 -- handed to the consumer
             q.put(e)
 
-    th = threading.Thread(target=produce, name="p265fe-parse", daemon=True)
-    th.start()
-    contexts = {}
-    pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
-    outq = OutputQueue()
-    inflight = collections.deque()
-    rank = 0
+    lanes = {}                          # params bytes -> [_Lane] * depth
+    k_submit = [0]
+
+    def lanes_for(params):
+        key = params.tobytes()
+        ls = lanes.get(key)
+        if ls is None:
+            t0 = clock()
+            ls = lanes[key] = [_Lane(*_context(params, device, 1)) for _ in range(depth)]
+            st.add("context", clock() - t0)
+        return ls
 
     def submit(group):
-        key = group[0].params.tobytes()
-        ctx = contexts.get(key)
-        if ctx is None:
+        lane = lanes_for(group[0].params)[k_submit[0] % depth]
+        k_submit[0] += 1
+        slots.acquire()                 # at most `depth` batches between upload and download
+        if stop.is_set():
+            slots.release()
+            return
+        with lane.lock:
             t0 = clock()
-            ck, ctx = _context(group[0].params, device, depth)
-            contexts[key] = (ck, ctx)
-            st.add("context", clock() - t0)
-        else:
-            ctx = ctx[1]
-        t0 = clock()
-        b = ctx.upload([d.picture for d in group])          # records -> HBM (upload stream)
-        t1 = clock()
-        ctx.run(b)                                          # enqueued; runs while the host goes on
+            b = lane.ctx.upload([d.picture for d in group])     # records -> HBM
+            t1 = clock()
+            lane.ctx.run(b)                                     # enqueued; decodes meanwhile
         st.add("upload", t1 - t0)
         st.add("run_enqueue", clock() - t1)
-        inflight.append((ctx, b, group))
+        done_q.put((lane, b, group))
 
-    def retire():
-        ctx, b, group = inflight.popleft()
-        t0 = clock()
-        outs = ctx.download(b)                              # waits for the batch, planes -> host
-        st.add("download_wait", clock() - t0)
-        b.free()
+    def submitter():
+        try:
+            pending = []
+            while True:
+                t0 = clock()
+                item = q.get()
+                st.add("wait_parser", clock() - t0)
+                if isinstance(item, BaseException):
+                    raise item
+                end = item is None
+                for d in item or []:
+                    if pending and (len(pending) >= batch or d.params.tobytes() != pending[0].params.tobytes()):
+                        submit(pending)
+                        pending = []
+                    pending.append(d)
+                # the parser has nothing ready right now: decode what is pending instead of waiting
+                if pending and (end or (q.empty() and len(pending) >= min_batch)):
+                    submit(pending)
+                    pending = []
+                if end or stop.is_set():
+                    break
+            done_q.put(None)
+        except BaseException as e:  # noqa: BLE001 -- handed to the consumer
+            done_q.put(e)
+
+    th_p = threading.Thread(target=produce, name="p265fe-parse", daemon=True)
+    th_s = threading.Thread(target=submitter, name="p265r-submit", daemon=True)
+    th_p.start()
+    th_s.start()
+    pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
+    outq = OutputQueue()
+    rank = 0
+
+    def retire(lane, b, group):
+        with lane.lock:
+            t0 = clock()
+            outs = lane.ctx.download(b)                         # waits for the batch, planes -> host
+            st.add("download_wait", clock() - t0)
+            b.free()
+        slots.release()
         ready = []
         for d, planes in zip(group, outs):
             fr = DecodedFrame(poc=d.poc, output_rank=-1, decode_index=int(d.picture.meta["decode_index"]),
@@ -221,57 +271,54 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 16, thr
         return fr
 
     try:
-        pending = []
         while True:
             t0 = clock()
-            item = q.get()
-            st.add("wait_parser", clock() - t0)
+            item = done_q.get()
+            st.add("wait_submit", clock() - t0)
             if isinstance(item, BaseException):
                 raise item
-            end = item is None
-            for d in item or []:
-                if pending and (len(pending) >= batch or d.params.tobytes() != pending[0].params.tobytes()):
-                    submit(pending)
-                    pending = []
-                    while len(inflight) >= depth:
-                        for it in retire():
-                            yield emit(it)
-                pending.append(d)
-            # the parser has nothing ready right now: decode what is pending instead of waiting
-            if pending and (end or (q.empty() and len(pending) >= min_batch)):
-                submit(pending)
-                pending = []
-                while len(inflight) >= depth:
-                    for it in retire():
-                        yield emit(it)
-            if end:
+            if item is None:
                 break
-        while inflight:
-            for it in retire():
+            for it in retire(*item):
                 yield emit(it)
         for it in outq.flush():
             yield emit(it)
     finally:
         stop.set()
-        while th.is_alive():
+        for _ in range(depth):
+            slots.release()             # a submitter blocked on a slot sees `stop`
+        while th_p.is_alive() or th_s.is_alive():
+            for qq in (q, done_q):
+                try:
+                    left = qq.get(timeout=0.02)
+                except queue.Empty:
+                    continue
+                if isinstance(left, tuple) and len(left) == 3:
+                    lane, b, _ = left
+                    with lane.lock:
+                        b.free()
+        while True:                     # batches submitted but never retired
             try:
-                q.get(timeout=0.05)
+                left = done_q.get_nowait()
             except queue.Empty:
-                pass
+                break
+            if isinstance(left, tuple) and len(left) == 3:
+                lane, b, _ = left
+                with lane.lock:
+                    b.free()
         pool.shutdown(wait=True)
-        for ctx, b, _ in inflight:
-            b.free()
         t0 = clock()
-        for ck, ctx in contexts.values():
-            if cache_contexts:
-                _return_context(ck, ctx)
-            else:
-                ctx.close()
+        for ls in lanes.values():
+            for lane in ls:
+                if cache_contexts:
+                    _return_context(lane.key, lane.ctx)
+                else:
+                    lane.ctx.close()
         st.add("context", clock() - t0)
 
 
-def decode_bytes(data: bytes, device: int = 0, batch: int = 16, threads: int = 0,
-                 verify_hash: bool = True, chunk: int = 1 << 20, **kw) -> List[DecodedFrame]:
+def decode_bytes(data: bytes, device: int = 0, batch: int = 8, threads: int = 0,
+                 verify_hash: bool = True, chunk: int = 2 << 20, **kw) -> List[DecodedFrame]:
     """Decode a whole stream held in memory; returns the output pictures in output order."""
     return list(decode_chunks(_chunks(data, chunk), device=device, batch=batch, threads=threads,
                               verify_hash=verify_hash, **kw))

@@ -118,3 +118,18 @@ def test_c5_tile_units_on_the_gpu(dec_mod):
                 planes.append(ctx.decode([tpic])[0])
         full = tiles.stitch(p.params, parts, planes)
         assert [hashlib.md5(full[c].tobytes()).digest() for c in range(3)] == p.hash
+
+
+def test_decoder_abandoned_midway_ends_its_threads(dec_mod):
+    """Leaving the decode_chunks generator after one frame (or on an exception) stops the parse
+    and submit threads and frees the batches in flight: no hang, and the next decode works."""
+    import threading
+    data = open(os.path.join(GOLDEN, "synth_1080p_4pic.bin"), "rb").read() * 4
+    before = threading.active_count()
+    gen = dec_mod.decode_chunks([data[i:i + 100000] for i in range(0, len(data), 100000)], batch=2, depth=2)
+    first = next(gen)
+    assert first.hash_ok
+    gen.close()
+    assert threading.active_count() <= before + 1            # (the hash pool's threads are gone too)
+    frames = dec_mod.decode_bytes(data[:len(data) // 4])
+    assert len(frames) == 4 and all(f.hash_ok for f in frames)

@@ -26,14 +26,19 @@ print("parse alone: %.3f s  %.0f CTU/s" % (parse_s, n_ctu / parse_s))
 decoder.decode_bytes(one)                                    # warm: contexts, kernels
 rows = []
 MB = 1 << 20
-for batch, depth, chunk in [(16, 1, MB), (16, 2, 4 * MB), (16, 2, 16 * MB), (32, 2, 4 * MB), (16, 3, 4 * MB),
-                            (8, 2, 4 * MB), (32, 1, 16 * MB)]:
-    st = decoder.StageTimes()
-    t = time.perf_counter()
-    frames = decoder.decode_bytes(data, batch=batch, threads=threads, depth=depth, stats=st, chunk=chunk)
-    dt = time.perf_counter() - t
-    assert len(frames) == len(pics) and all(f.hash_ok for f in frames)
+configs = [(8, 2, 2 * MB), (8, 3, 2 * MB), (4, 3, 2 * MB), (8, 2, 1 * MB), (16, 2, 2 * MB), (8, 4, 2 * MB),
+           (12, 3, 2 * MB)]
+for batch, depth, chunk in configs:
+    best = None
+    for rep in range(2):
+        st = decoder.StageTimes()
+        t = time.perf_counter()
+        frames = decoder.decode_bytes(data, batch=batch, threads=threads, depth=depth, stats=st, chunk=chunk)
+        dt = time.perf_counter() - t
+        assert len(frames) == len(pics) and all(f.hash_ok for f in frames)
+        if best is None or dt < best[0]:
+            best = (dt, st)
+    dt, st = best
     row = {"batch": batch, "depth": depth, "chunk_mb": chunk // MB, "e2e_s": round(dt, 4), "e2e_ctu_s": round(n_ctu / dt),
            **{k: round(v, 4) for k, v in sorted(st.items())}}
-    rows.append(row)
-    print(json.dumps(row))
+    print(json.dumps(row), flush=True)
