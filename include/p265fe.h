@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define P265FE_ABI_VERSION 2u
+#define P265FE_ABI_VERSION 3u   /* 3: P265FE_ASYNC, p265fe_wait */
 
 #define P265FE_OK            0
 #define P265FE_EINVAL       -1   /* bad argument                                   */
@@ -58,6 +58,8 @@ extern "C" {
 
 /* p265fe_feed flags */
 #define P265FE_FLUSH          1   /* end of stream: the last access unit is complete */
+#define P265FE_ASYNC          2   /* parse the complete access units on the decoder's persistent
+                                     workers and return at once (p265fe_wait / p265fe_take) */
 
 typedef struct p265fe_picture_info {
     p265r_params     params;        /* back-end parameters of this picture's SPS/PPS         */
@@ -109,6 +111,15 @@ int  p265fe_feed(p265fe_decoder* dec, const uint8_t* data, size_t size, int n_th
  * size.  output_rank is -1 in a set: output order is the caller's (cvs_id, poc,
  * max_num_reorder, output_flag give what the bumping process needs). */
 int  p265fe_take(p265fe_decoder* dec, p265fe_pictures** out);
+/* P265FE_ASYNC: every feed of a decoder passes it (no mixing).  Access units are parsed in the
+ * background on n_threads persistent workers (those of the first async feed), so parsing of a
+ * chunk overlaps the slowest pictures of the previous one; p265fe_feed returns the number of
+ * pictures submitted and not yet taken.  p265fe_take then hands out the PARSED PREFIX in decode
+ * order (possibly empty; a picture that failed to parse ends the prefix and its error code is
+ * returned once the pictures before it are taken).  p265fe_wait blocks until the next picture in
+ * decode order is parsed (all = 0) or every submitted one is (all = 1), and returns how many are
+ * ready to take. */
+int  p265fe_wait(p265fe_decoder* dec, int all);
 int  p265fe_pictures_get(const p265fe_pictures* set, int i, p265fe_picture_info* out);
 void p265fe_pictures_free(p265fe_pictures* set);
 

@@ -29,10 +29,11 @@ from . import records as R
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("P265FE_LIB", os.path.join(HERE, "libp265fe.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, EINVAL, ENOMEM, EUNSUPPORTED, EBITSTREAM = 0, -1, -2, -4, -8
 HASH_NONE, HASH_MD5, HASH_CRC, HASH_CHECKSUM = -1, 0, 1, 2
 FLUSH = 1
+ASYNC = 2                       # p265fe_feed: P265FE_ASYNC
 
 
 class BitstreamError(ValueError):
@@ -62,6 +63,7 @@ SIGNATURES = {
     "p265fe_picture": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PictureInfoC)]),
     "p265fe_feed": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
     "p265fe_take": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "p265fe_wait": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265fe_pictures_get": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PictureInfoC)]),
     "p265fe_pictures_free": (None, [_vp]),
     "p265fe_last_error": (ctypes.c_char_p, [_vp]),
@@ -231,9 +233,14 @@ class StreamParser:
     ``feed(chunk)`` returns the pictures completed so far, in decode order; stream state
     (parameter sets, POC, a partial access unit or NAL unit) carries over between calls;
     ``feed(b"", flush=True)`` ends the stream.  Output order is the caller's (see
-    decoder.OutputQueue): ``output_rank`` stays -1 here."""
+    decoder.OutputQueue): ``output_rank`` stays -1 here.
 
-    def __init__(self, threads: int = 0, validate: bool = False):
+    ``asynchronous=True`` (P265FE_ASYNC): ``feed`` only submits the complete access units to the
+    decoder's persistent parse workers and returns the pictures parsed so far (a decode-order
+    prefix, possibly empty); ``wait(all)`` blocks for the next one (or all) and returns them, so
+    the parsing of one chunk overlaps the slowest pictures of the previous one."""
+
+    def __init__(self, threads: int = 0, validate: bool = False, asynchronous: bool = False):
         self.lib = load()
         h = ctypes.c_void_p()
         if self.lib.p265fe_create(ctypes.byref(h)) != OK:
@@ -242,20 +249,43 @@ class StreamParser:
         self.h = h
         self.threads = int(threads)
         self.validate = validate
+        self.asynchronous = bool(asynchronous)
         self.n_pictures = 0
+        self.pending = 0            # async: submitted and not yet taken
 
     def feed(self, data: bytes, flush: bool = False):
         lib = self.lib
         data = bytes(data)
-        n = lib.p265fe_feed(self.h, data, len(data), self.threads, FLUSH if flush else 0)
+        flags = (FLUSH if flush else 0) | (ASYNC if self.asynchronous else 0)
+        n = lib.p265fe_feed(self.h, data, len(data), self.threads, flags)
         if n < 0:
             _fail(lib, self.h, n, "p265fe_feed")
+        if self.asynchronous:
+            self.pending = n
+        return self._take()
+
+    def wait(self, all: bool = False):
+        """Async: block until the next picture in decode order is parsed (or every submitted one,
+        ``all``), then take the parsed prefix ([] when nothing is pending)."""
+        if not self.pending:
+            return []
+        n = self.lib.p265fe_wait(self.h, 1 if all else 0)
+        if n < 0:
+            _fail(self.lib, self.h, n, "p265fe_wait")
+        return self._take()
+
+    def _take(self):
+        lib = self.lib
         sp = ctypes.c_void_p()
         cnt = lib.p265fe_take(self.h, ctypes.byref(sp))
         if cnt < 0:
+            if cnt in (EBITSTREAM, EUNSUPPORTED):
+                _fail(lib, self.h, cnt, "p265fe_take")
             raise MemoryError("p265fe_take failed (%d)" % cnt)
         owner = _SetOwner(lib, sp)
         pics = _collect(lambda i, ref: lib.p265fe_pictures_get(sp, i, ref), cnt, owner, self.validate,
                         base=self.n_pictures)
         self.n_pictures += cnt
+        if self.asynchronous:
+            self.pending -= cnt
         return pics

@@ -6,7 +6,9 @@
 // being assembled and an incomplete trailing NAL unit carry over between calls.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -86,10 +88,100 @@ struct p265fe_pictures {
     std::vector<PictureRecords> recs;
 };
 
+// Asynchronous slice-data parsing (P265FE_ASYNC): complete access units go to persistent workers;
+// the decoder hands them out in decode order as the prefix of parsed pictures grows, so parsing of
+// later chunks overlaps the stragglers of earlier ones (no per-chunk join).
+struct AsyncParser {
+    struct Slot {
+        std::unique_ptr<PictureJob> job;
+        PictureRecords rec;
+        int state = 0;                          // 0 queued, 1 parsing, 2 done
+        int code = 0;
+        std::string msg;
+    };
+    std::mutex m;
+    std::condition_variable cv_work, cv_done;
+    std::deque<std::unique_ptr<Slot>> slots;    // submitted, not yet taken, decode order
+    size_t next_work = 0;                       // slots[0 .. next_work) handed to a worker
+    uint64_t base = 0;                          // decode index of slots[0]
+    std::vector<std::thread> workers;
+    bool quit = false;
+
+    void start(int n) {
+        if (!workers.empty()) return;
+        for (int t = 0; t < std::max(1, n); ++t) workers.emplace_back([this] { run(); });
+    }
+    void run() {
+        for (;;) {
+            Slot* sl = nullptr;
+            uint64_t idx = 0;
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv_work.wait(g, [&] { return quit || next_work < slots.size(); });
+                if (quit) return;
+                sl = slots[next_work].get();
+                idx = base + next_work;
+                ++next_work;
+                sl->state = 1;
+            }
+            PictureJob& j = *sl->job;
+            std::vector<SliceRef> sr;
+            for (size_t k = 0; k < j.slices.size(); ++k)
+                sr.push_back(SliceRef{j.hdrs[k].get(), j.slices[k].rbsp.data(), j.slices[k].rbsp.size()});
+            int code = 0;
+            std::string msg;
+            try {
+                decode_picture(*j.act, sr, sl->rec);
+            } catch (const Unsupported& e) {
+                code = P265FE_EUNSUPPORTED; msg = e.what();
+            } catch (const BitstreamError& e) {
+                code = P265FE_EBITSTREAM; msg = e.what();
+            } catch (const std::bad_alloc&) {
+                code = P265FE_ENOMEM; msg = "out of memory";
+            } catch (const std::exception& e) {
+                code = P265FE_EBITSTREAM; msg = e.what();
+            }
+            {
+                std::lock_guard<std::mutex> g(m);
+                sl->code = code;
+                if (code) sl->msg = "picture " + std::to_string(idx) + ": " + msg;
+                sl->state = 2;
+            }
+            cv_done.notify_all();
+        }
+    }
+    void submit(std::vector<std::unique_ptr<PictureJob>>& jobs) {
+        {
+            std::lock_guard<std::mutex> g(m);
+            for (auto& j : jobs) {
+                auto sl = std::make_unique<Slot>();
+                sl->job = std::move(j);
+                slots.push_back(std::move(sl));
+            }
+        }
+        jobs.clear();
+        cv_work.notify_all();
+    }
+    size_t done_prefix_locked() const {
+        size_t k = 0;
+        while (k < slots.size() && slots[k]->state == 2) ++k;
+        return k;
+    }
+    ~AsyncParser() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            quit = true;
+        }
+        cv_work.notify_all();
+        for (auto& t : workers) t.join();
+    }
+};
+
 struct p265fe_decoder {
     StreamState st;
     p265fe_pictures ready;                    // parsed, not yet taken
     p265fe_pictures* last = nullptr;          // result of p265fe_decode (p265fe_picture)
+    std::unique_ptr<AsyncParser> async;       // P265FE_ASYNC feeds
     std::string err;
 };
 
@@ -315,7 +407,9 @@ void p265fe_destroy(p265fe_decoder* d) {
 const char* p265fe_last_error(p265fe_decoder* d) { return d ? d->err.c_str() : ""; }
 
 int p265fe_feed(p265fe_decoder* d, const uint8_t* data, size_t size, int n_threads, int flags) {
-    if (!d || (!data && size) || (flags & ~P265FE_FLUSH)) return P265FE_EINVAL;
+    if (!d || (!data && size) || (flags & ~(P265FE_FLUSH | P265FE_ASYNC))) return P265FE_EINVAL;
+    const bool async = (flags & P265FE_ASYNC) != 0;
+    if (async != (d->async != nullptr) && (d->async || !d->ready.jobs.empty())) return P265FE_EINVAL;   // no mixing
     d->err.clear();
     StreamState& st = d->st;
     try {
@@ -335,6 +429,13 @@ int p265fe_feed(p265fe_decoder* d, const uint8_t* data, size_t size, int n_threa
         std::vector<Nal> nals = split_nals(buf.data(), cut);
         for (auto& nal : nals) process_nal(st, std::move(nal));
         if (flags & P265FE_FLUSH) finish_current(st);
+        if (async) {
+            if (!d->async) d->async = std::make_unique<AsyncParser>();
+            d->async->start(n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency()));
+            d->async->submit(st.complete);
+            std::lock_guard<std::mutex> g(d->async->m);
+            return (int)d->async->slots.size();
+        }
         int rc = parse_pictures(st.complete, d->ready, n_threads, d->err);
         if (rc) return rc;
         return (int)d->ready.jobs.size();
@@ -354,12 +455,44 @@ int p265fe_take(p265fe_decoder* d, p265fe_pictures** out) {
     *out = nullptr;
     auto* set = new (std::nothrow) p265fe_pictures();
     if (!set) return P265FE_ENOMEM;
+    if (d->async) {                             // the parsed prefix, decode order; stop at an error
+        AsyncParser& a = *d->async;
+        std::lock_guard<std::mutex> g(a.m);
+        const size_t n = a.done_prefix_locked();
+        size_t k = 0;
+        for (; k < n; ++k) {
+            if (a.slots[k]->code) break;
+            set->jobs.push_back(std::move(a.slots[k]->job));
+            set->recs.push_back(std::move(a.slots[k]->rec));
+        }
+        const int code = k < n ? a.slots[k]->code : 0;
+        if (code) d->err = a.slots[k]->msg;
+        for (size_t i = 0; i < k; ++i) a.slots.pop_front();
+        a.base += k;
+        a.next_work -= k;
+        if (code && set->jobs.empty()) { delete set; return code; }
+        *out = set;
+        return (int)set->jobs.size();
+    }
     set->jobs = std::move(d->ready.jobs);
     set->recs = std::move(d->ready.recs);
     d->ready.jobs.clear();
     d->ready.recs.clear();
     *out = set;
     return (int)set->jobs.size();
+}
+
+int p265fe_wait(p265fe_decoder* d, int all) {
+    if (!d) return P265FE_EINVAL;
+    if (!d->async) return (int)d->ready.jobs.size();
+    AsyncParser& a = *d->async;
+    std::unique_lock<std::mutex> g(a.m);
+    a.cv_done.wait(g, [&] {
+        const size_t n = a.done_prefix_locked();
+        if (all) return n == a.slots.size();
+        return a.slots.empty() || n > 0;
+    });
+    return (int)a.done_prefix_locked();
 }
 
 int p265fe_pictures_get(const p265fe_pictures* set, int i, p265fe_picture_info* out) {
@@ -372,6 +505,7 @@ void p265fe_pictures_free(p265fe_pictures* set) { delete set; }
 
 int p265fe_decode(p265fe_decoder* d, const uint8_t* data, size_t size, int n_threads) {
     if (!d || (!data && size)) return P265FE_EINVAL;
+    d->async.reset();
     d->st = StreamState();
     d->ready = p265fe_pictures();
     delete d->last;

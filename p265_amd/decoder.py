@@ -129,6 +129,22 @@ def release_contexts():
         c.close()
 
 
+def host_threads(cap=16):
+    """This process's CPU share: affinity, cgroup quota, OMP_NUM_THREADS (the GPU pool announces
+    its per-GPU share there), at most ``cap``."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(cap, n))
+
+
 class _Lane:
     """One back-end context of the decoder and the lock that serialises its calls: the submit
     thread uploads into it while the consumer downloads from another one (contexts are not
@@ -152,7 +168,9 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 8, thre
     between calls (``cache_contexts``; ``release_contexts()`` frees them)."""
     import time
     clock = time.perf_counter
-    parser = bitstream.StreamParser(threads=threads)
+    if not threads:
+        threads = host_threads()
+    parser = bitstream.StreamParser(threads=threads, asynchronous=True)
     q = queue.Queue(maxsize=max(1, prefetch))
     done_q = queue.Queue()
     slots = threading.Semaphore(max(1, depth))
@@ -161,20 +179,30 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 8, thre
     depth = max(1, min(4, depth))
 
     def produce():
+        # asynchronous parsing: feed() submits the complete access units to the parser's workers
+        # and returns the parsed prefix; the number of pictures in the parser is bounded
         try:
+            limit = max(8, 3 * (threads or 16))
             for ch in chunks:
                 if stop.is_set():
                     q.put(None)         # the submitter ends on it (the consumer drains q)
                     return
-                t0 = clock()
                 pics = parser.feed(ch)
-                st.add("parse_thread_busy", clock() - t0)
                 if pics:
                     q.put(pics)
-            t0 = clock()
-            last = parser.feed(b"", flush=True)
-            st.add("parse_thread_busy", clock() - t0)
-            q.put(last)
+                while parser.pending > limit and not stop.is_set():
+                    t0 = clock()
+                    pics = parser.wait()
+                    st.add("parse_backpressure", clock() - t0)
+                    if pics:
+                        q.put(pics)
+            pics = parser.feed(b"", flush=True)
+            if pics:
+                q.put(pics)
+            while parser.pending and not stop.is_set():
+                pics = parser.wait()
+                if pics:
+                    q.put(pics)
             q.put(None)
         except BaseException as e:  # noqa: BLE001 -- handed to the consumer
             q.put(e)
@@ -236,7 +264,7 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 8, thre
     th_s = threading.Thread(target=submitter, name="p265r-submit", daemon=True)
     th_p.start()
     th_s.start()
-    pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
+    pool = ThreadPoolExecutor(max_workers=threads)
     outq = OutputQueue()
     rank = 0
 

@@ -122,3 +122,52 @@ def test_streaming_errors():
     with pytest.raises(bitstream.BitstreamError):
         p.feed(data[5000:9000], flush=True)                      # picture 0 ends truncated
     assert bitstream.StreamParser().feed(b"\x00\x00", flush=True) == []
+
+
+def _feed_all_async(data, sizes, threads=3):
+    p = bitstream.StreamParser(threads=threads, asynchronous=True)
+    out, pos, i = [], 0, 0
+    while pos < len(data):
+        n = sizes[i % len(sizes)]
+        out += p.feed(data[pos:pos + n])
+        if i % 3 == 2:
+            out += p.wait()                      # sometimes block for the next picture
+        pos += n
+        i += 1
+    out += p.feed(b"", flush=True)
+    out += p.wait(all=True)
+    assert p.pending == 0 and p.wait() == []
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(STREAMS))
+def test_async_feed_equals_one_shot(name):
+    """P265FE_ASYNC: pictures parsed in the background by persistent workers come out in decode
+    order, identical to the one-shot parse, whatever the chunking."""
+    data = STREAMS[name]()
+    ref = bitstream.decode_stream(data, threads=2)
+    for sizes in ([len(data)], [997], [1, 5000, 37], [20000]):
+        got = _feed_all_async(data, sizes)
+        assert len(got) == len(ref)
+        for a, b in zip(got, ref):
+            _same(a, b)
+
+
+def test_async_feed_reports_a_broken_picture_in_order():
+    """A picture that fails to parse ends the parsed prefix: the pictures before it are handed
+    out, then its error is raised."""
+    data = bytearray(STREAMS["idr_period"]())
+    ref = bitstream.decode_stream(bytes(data))
+    # corrupt the slice data of the third picture (after its slice header)
+    starts = [i for i in range(len(data) - 3) if data[i:i + 3] == b"\x00\x00\x01" and (data[i + 3] >> 1) & 63 in (19, 20, 1)]
+    k = starts[2] + 40
+    data[k:k + 200] = b"\xff" * 200
+    p = bitstream.StreamParser(threads=2, asynchronous=True)
+    got = []
+    with pytest.raises(bitstream.BitstreamError):
+        got += p.feed(bytes(data), flush=True)
+        while p.pending:
+            got += p.wait()
+    assert len(got) <= 2 and len(ref) >= 3
+    for a, b in zip(got, ref):
+        _same(a, b)
