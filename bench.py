@@ -283,15 +283,19 @@ def end_to_end(device, reps=16, threads=16):
     pics = bitstream.decode_stream(data, threads=threads)
     fe_s = time.perf_counter() - t0
     n_ctu = sum(len(p.picture.ctus) for p in pics)
-    decoder.decode_bytes(one, device=device)                       # warm (contexts, kernels)
+    decoder.decode_bytes(one, device=device, threads=threads)      # warm (contexts, kernels)
     t0 = time.perf_counter()
-    frames = decoder.decode_bytes(data, device=device, batch=64, threads=threads)
+    frames = decoder.decode_bytes(data, device=device, threads=threads)
     e2e_s = time.perf_counter() - t0
+    decoder.release_contexts()
     return {"stream": "tests/golden/synth_1080p_4pic.bin x%d" % reps, "pictures": len(pics), "ctus": n_ctu,
             "bytes_per_ctu": round(len(one) * reps / n_ctu, 1), "threads": threads,
             "frontend_ctu_s": round(n_ctu / fe_s, 1), "frontend_mb_s": round(len(data) / fe_s / 1e6, 2),
             "e2e_ctu_s": round(n_ctu / e2e_s, 1),
             "hash_checked": sum(1 for f in frames if f.hash_ok), "hash_failed": sum(1 for f in frames if f.hash_ok is False),
+            "config": "decoder.decode_bytes defaults: %d-picture batches over %d warm contexts, %d MB chunks, "
+                      "asynchronous parse on %d threads" % (decoder.DEFAULT_BATCH, decoder.DEFAULT_DEPTH,
+                                                             decoder.DEFAULT_CHUNK >> 20, threads),
             "note": "native front-end (libp265fe.so) on host threads + PCIe-inclusive GPU decode; not `value`"}
 
 

@@ -21,8 +21,9 @@ def parse_cmd(argv=None):
     ap.add_argument("-o", "--output", help="The reconstructed YUV output (I420, cropped, output order).")
     ap.add_argument("--skip-syntax-dump", type=int, default=0, help="Accepted for compatibility; no effect.")
     ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--threads", type=int, default=0, help="front-end parsing threads (0 = all cores)")
-    ap.add_argument("--batch", type=int, default=64, help="pictures per GPU batch")
+    ap.add_argument("--threads", type=int, default=0, help="front-end parsing threads (0 = this process's CPU share, <= 16)")
+    ap.add_argument("--batch", type=int, default=decoder.DEFAULT_BATCH, help="pictures per GPU batch")
+    ap.add_argument("--depth", type=int, default=decoder.DEFAULT_DEPTH, help="GPU batches in flight (one warm context each)")
     ap.add_argument("--no-verify", action="store_true", help="do not fail on a decoded picture hash mismatch")
     return ap.parse_args(argv)
 
@@ -31,7 +32,7 @@ def main(argv=None):
     a = parse_cmd(argv)
     t0 = time.time()
     st = decoder.decode_file(a.bitstream, a.output, device=a.device, batch=a.batch, threads=a.threads,
-                             verify_hash=not a.no_verify)
+                             depth=a.depth, verify_hash=not a.no_verify)
     dt = time.time() - t0
     print("decoded %d pictures in %.3f s; picture hash SEI checked %d, mismatched %d"
           % (st["pictures"], dt, st["hash_checked"], st["hash_mismatch"]))

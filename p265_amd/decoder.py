@@ -154,8 +154,12 @@ class _Lane:
         self.key, self.ctx, self.lock = key, ctx, threading.Lock()
 
 
-def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 8, threads: int = 0,
-                  verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4, depth: int = 2,
+# end-to-end defaults (tools/e2e_profile.py sweep on the GPU box, 64 x 1080p, 16 host threads)
+DEFAULT_BATCH, DEFAULT_DEPTH, DEFAULT_CHUNK = 8, 2, 1 << 20
+
+
+def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT_BATCH, threads: int = 0,
+                  verify_hash: bool = True, min_batch: int = 8, prefetch: int = 4, depth: int = DEFAULT_DEPTH,
                   stats: Optional[StageTimes] = None, cache_contexts: bool = True) -> Iterator[DecodedFrame]:
     """Decode a stream given as an iterable of byte chunks; yields frames in output order.
 
@@ -345,8 +349,8 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = 8, thre
         st.add("context", clock() - t0)
 
 
-def decode_bytes(data: bytes, device: int = 0, batch: int = 8, threads: int = 0,
-                 verify_hash: bool = True, chunk: int = 2 << 20, **kw) -> List[DecodedFrame]:
+def decode_bytes(data: bytes, device: int = 0, batch: int = DEFAULT_BATCH, threads: int = 0,
+                 verify_hash: bool = True, chunk: int = DEFAULT_CHUNK, **kw) -> List[DecodedFrame]:
     """Decode a whole stream held in memory; returns the output pictures in output order."""
     return list(decode_chunks(_chunks(data, chunk), device=device, batch=batch, threads=threads,
                               verify_hash=verify_hash, **kw))
