@@ -41,6 +41,9 @@ using namespace p265r;
 #ifndef P265R_EXPERIMENTS
 #define P265R_EXPERIMENTS 0
 #endif
+#ifndef P265R_SPLIT_W16
+#define P265R_SPLIT_W16 1          // small split batches: W = 16 row kernel (0: the by-run W, A/B)
+#endif
 
 namespace {
 
@@ -385,6 +388,12 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 6) return launch_rows_w<6, 1>(ctx, b, st, alone);
     if (ctx->lean == 0 && (ctx->row_waves == 8 || (ctx->row_waves == 0 && !alone))) return launch_rows_w<8, 1>(ctx, b, st, alone);
 #endif
+    // a batch small enough for the component split with one workgroup per CU (the latency regime:
+    // tile units, the decoder's small batches): W = 16, so every CTU row of a picture's chain can
+    // be in flight at once (a 2-CTU-lag wavefront of 17 rows needs 17 waves; with 12 the rows
+    // after the 12th wait for a whole row to finish)
+    if (ctx->row_waves == 0 && ctx->split && P265R_SPLIT_W16 && 2 * (long long)b->n_pics <= ctx->num_cus)
+        return launch_rows_w<16, 4>(ctx, b, st, alone);
     const int w = ctx->row_waves ? ctx->row_waves : (alone ? 12 : 8);
     return w == 12 ? launch_rows_w<12, 6>(ctx, b, st, alone) : launch_rows_w<8, 6>(ctx, b, st, alone);
 }

@@ -365,7 +365,7 @@ def _file_chunks(path, chunk):
             yield b
 
 
-def decode_file(path: str, output: Optional[str] = None, chunk: int = 8 << 20, **kw) -> dict:
+def decode_file(path: str, output: Optional[str] = None, chunk: int = DEFAULT_CHUNK, **kw) -> dict:
     """Stream a bitstream file to a cropped I420 YUV file in output order; returns counts."""
     n = checked = bad = 0
     f = open(output, "wb") if output else None
