@@ -33,6 +33,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# the C oracle (output check, CPU baseline) runs OpenMP regions: passive waiting, so its idle
+# workers do not spin on the cores the end-to-end leg's parse threads use afterwards
+os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "reconstructed CTUs/sec (1080p all-intra) + achieved HBM GB/s vs peak"
@@ -284,14 +287,19 @@ def end_to_end(device, reps=16, threads=16):
     fe_s = time.perf_counter() - t0
     n_ctu = sum(len(p.picture.ctus) for p in pics)
     decoder.decode_bytes(one, device=device, threads=threads)      # warm (contexts, kernels)
-    t0 = time.perf_counter()
-    frames = decoder.decode_bytes(data, device=device, threads=threads)
-    e2e_s = time.perf_counter() - t0
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        frames = decoder.decode_bytes(data, device=device, threads=threads)
+        runs.append(time.perf_counter() - t0)
+        if not all(f.hash_ok for f in frames):
+            break
+    e2e_s = min(runs)
     decoder.release_contexts()
     return {"stream": "tests/golden/synth_1080p_4pic.bin x%d" % reps, "pictures": len(pics), "ctus": n_ctu,
             "bytes_per_ctu": round(len(one) * reps / n_ctu, 1), "threads": threads,
             "frontend_ctu_s": round(n_ctu / fe_s, 1), "frontend_mb_s": round(len(data) / fe_s / 1e6, 2),
-            "e2e_ctu_s": round(n_ctu / e2e_s, 1),
+            "e2e_ctu_s": round(n_ctu / e2e_s, 1), "e2e_runs_s": [round(r, 4) for r in runs],
             "hash_checked": sum(1 for f in frames if f.hash_ok), "hash_failed": sum(1 for f in frames if f.hash_ok is False),
             "config": "decoder.decode_bytes defaults: %d-picture batches over %d warm contexts, %d MB chunks, "
                       "asynchronous parse on %d threads" % (decoder.DEFAULT_BATCH, decoder.DEFAULT_DEPTH,
