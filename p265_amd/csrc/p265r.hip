@@ -159,6 +159,7 @@ struct p265r_batch {
     int16_t* d_res = nullptr;
     int* d_err = nullptr;
     ResJob* d_jobs[RC_NUM] = {};
+    uint32_t slab[RC_NUM] = {};    // int16 offset of each class's packed TBs in the pool (fixed-size classes)
     BatchView view{};
     int n_jobs[RC_NUM] = {};
     std::vector<DevPic> h_pics;
@@ -704,7 +705,11 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
     b->d_res = reinterpret_cast<int16_t*>(dbase + o_res);
     b->d_err = reinterpret_cast<int*>(dbase + o_err);
-    for (int c = 0; c < RC_NUM; ++c) { b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]); b->n_jobs[c] = n_jobs[c]; }
+    for (int c = 0; c < RC_NUM; ++c) {
+        b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]);
+        b->n_jobs[c] = n_jobs[c];
+        b->slab[c] = (uint32_t)pool_base[c];
+    }
     b->h_pics.resize(n_pics);
 
     P265R_UT("alloc");
@@ -897,23 +902,23 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], ps));
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
-        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl);
+        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT4]) {
-        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc);
+        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT8]) {
-        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc);
+        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT16]) {
-        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc);
+        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT32]) {
-        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc);
+        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_TSKIP]) {

@@ -78,16 +78,20 @@ __device__ __forceinline__ void inv4(const int (&c)[4], int (&o)[4]) {
     }
 }
 
+// A class's TBs are packed back to back in job order (p265r_batch_upload), so TB i of a fixed-size
+// class sits at slab + i * N * N: the coefficient loads do not wait for the job record (which
+// only supplies qP), one dependent memory round trip less per TB.
 template <bool DST>
 __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restrict__ pool,
                                                         int16_t* __restrict__ res,
                                                         const ResJob* __restrict__ jobs, int n_jobs,
-                                                        int bit_depth) {
+                                                        int bit_depth, uint32_t slab) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_jobs) return;
     const ResJob jb = jobs[i];
-    const int16_t* blk = pool + jb.off;
-    int16_t* dst = res + jb.off;
+    const size_t off = (size_t)slab + (size_t)i * 16;
+    const int16_t* blk = pool + off;
+    int16_t* dst = res + off;
     const uint4 raw0 = *reinterpret_cast<const uint4*>(blk);       // 16 x int16 = 32 B
     const uint4 raw1 = *reinterpret_cast<const uint4*>(blk + 8);
     const uint32_t w[8] = {raw0.x, raw0.y, raw0.z, raw0.w, raw1.x, raw1.y, raw1.z, raw1.w};
@@ -166,7 +170,7 @@ template <int LOG2>
 __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restrict__ pool,
                                                        int16_t* __restrict__ res,
                                                        const ResJob* __restrict__ jobs, int n_jobs,
-                                                       int bit_depth_luma, int bit_depth_chroma) {
+                                                       int bit_depth_luma, int bit_depth_chroma, uint32_t slab) {
     constexpr int N = 1 << LOG2;
     constexpr int TPB = 256 / N;                 // TBs per block
     constexpr int S = N + 2;                     // padded LDS row (odd dword stride)
@@ -177,8 +181,9 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
     const bool active = job < n_jobs;
     int16_t* t = tile[local];
     ResJob jb = active ? jobs[job] : ResJob{0, 0, 0, 0, 0};
-    const int16_t* blk = pool + jb.off;
-    int16_t* dst = res + jb.off;
+    const size_t off = (size_t)slab + (size_t)(active ? job : 0) * (N * N);   // (class slab, job order)
+    const int16_t* blk = pool + off;
+    int16_t* dst = res + off;
     const int bit_depth = jb.c_idx ? bit_depth_chroma : bit_depth_luma;
     if (active) {
         const Dequant dq(jb.qp, bit_depth + LOG2 - 5);
