@@ -452,8 +452,10 @@ def main():
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
                                         % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
-                     "note": "instruction-issue-bound (VALU + the CU's one scalar unit), not HBM-bound: see "
-                             "issue_rates and DESIGN.md §4"},
+                     "note": "bound by instruction issue (the CU's one scalar unit + each SIMD's VALU shared by "
+                             "24 waves; waves park on s_waitcnt 42 % of their cycles while others issue), not by "
+                             "HBM: halving the quad jobs' LDS round trips at +10-15 % instructions was 18 % slower "
+                             "(DESIGN.md §4, round 4); see issue_rates"},
         "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms),
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
         "phase_gbs": {"residual": round(res_b / (acc["residual_ms"] / a.steps * 1e-3) / 1e9, 1),
