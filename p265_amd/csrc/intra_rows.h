@@ -1126,6 +1126,22 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                     rn = issue(cur, t + 1);
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
+#ifdef P265R_PAD_SALU
+                {   // A/B probe: P265R_PAD_SALU dependent scalar adds per job (issue-bound test)
+                    uint32_t z = w0;
+#pragma unroll
+                    for (int q = 0; q < P265R_PAD_SALU; ++q) asm volatile("s_mov_b32 %0, %0" : "+s"(z));   // (s_mov: leaves SCC alone)
+                    asm volatile("" :: "s"(z));
+                }
+#endif
+#ifdef P265R_PAD_VALU
+                {   // A/B probe: P265R_PAD_VALU dependent vector adds per job
+                    uint32_t z = (uint32_t)lane;
+#pragma unroll
+                    for (int q = 0; q < P265R_PAD_VALU; ++q) asm volatile("v_add_u32 %0, 1, %0" : "+v"(z));
+                    asm volatile("" :: "v"(z));
+                }
+#endif
                 // Opaque copies of the lane id and the LDS bases: keeps the compiler from
                 // hoisting every template's lane-derived constants out of the job loop
                 // (7 inlined instances would otherwise hold them all live: ~150 VGPRs).

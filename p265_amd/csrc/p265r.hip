@@ -41,6 +41,9 @@ using namespace p265r;
 #ifndef P265R_EXPERIMENTS
 #define P265R_EXPERIMENTS 0
 #endif
+#ifndef P265R_EARLY_RESIDUAL
+#define P265R_EARLY_RESIDUAL 1     // re-runs: residual + prep start when the batch's previous intra phase ends
+#endif
 #ifndef P265R_SPLIT_W16
 #define P265R_SPLIT_W16 1          // small split batches: W = 16 row kernel (0: the by-run W, A/B)
 #endif
@@ -145,6 +148,8 @@ struct p265r_ctx {
     int fork_prep = 1;
     std::vector<hipStream_t> aux;     // aux[i]: lane i's prep stream (created on first use)
     std::vector<hipEvent_t> fork_ev, join_ev;
+    std::vector<hipStream_t> aux2;    // aux2[i]: lane i's residual stream (early residual phase)
+    std::vector<hipEvent_t> join2_ev;
     std::string describe;             // p265r_describe text
     unsigned char* dl_stage = nullptr;  // pinned download bounce buffer, 2 x kDlHalf (first download)
     hipEvent_t dl_ev[2] = {nullptr, nullptr};
@@ -171,6 +176,9 @@ struct p265r_batch {
     bool ragged = false;       // some picture is smaller than the context size (Geo::ragged)
     std::vector<std::array<int, 2>> size;   // per picture: luma width, height
     int runs = 0;              // p265r_batch_run calls so far
+    hipEvent_t intra_done = nullptr;   // recorded after each run's intra phase (the last reader of the
+                                       // residual pool and job lists): the next run's residual + prep
+                                       // phase waits for it instead of for the whole previous run
 };
 
 namespace {
@@ -522,8 +530,11 @@ void p265r_destroy(p265r_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     for (hipStream_t st : ctx->lanes) (void)hipStreamSynchronize(st);
     for (hipStream_t st : ctx->aux) if (st) (void)hipStreamSynchronize(st);
+    for (hipStream_t st : ctx->aux2) if (st) (void)hipStreamSynchronize(st);
     if (ctx->pending) p265r_batch_free(ctx, ctx->pending);
     for (hipStream_t st : ctx->aux) if (st) (void)hipStreamDestroy(st);
+    for (hipStream_t st : ctx->aux2) if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t e : ctx->join2_ev) if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->fork_ev) if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->join_ev) if (e) (void)hipEventDestroy(e);
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
@@ -871,6 +882,22 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     ctx->lane_busy |= 1u << b->lane;
     const bool prep = recon && ctx->schedule == 1 && !(skip & 2);
     hipStream_t ps = s;                              // the prep kernel's stream
+    // early residual phase (re-runs, no phase timing): the residual kernels and the job prep only
+    // overwrite what the batch's intra phase reads (residual pool, job lists, job counts), so they
+    // start as soon as the previous run's intra phase ends -- on two streams of the lane's own --
+    // and overlap the previous run's loop filters instead of queueing behind them
+    const bool early = P265R_EARLY_RESIDUAL && prep && ctx->fork_prep == 1 && !ctx->timing && b->intra_done && !(skip & 1);
+    hipStream_t rs = s;                              // the residual kernels' stream
+    if (early) {
+        const size_t li = (size_t)b->lane;
+        if (ctx->aux2.size() <= li) { ctx->aux2.resize(li + 1, nullptr); ctx->join2_ev.resize(li + 1, nullptr); }
+        if (!ctx->aux2[li]) {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->aux2[li], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->join2_ev[li], hipEventDisableTiming));
+        }
+        rs = ctx->aux2[li];
+        HIP_TRY(hipStreamWaitEvent(rs, b->intra_done, 0));
+    }
     if (prep && ctx->fork_prep) {
         // fork_prep 2: one prep stream shared by all lanes (fewer streams than HW queues, so no
         // lane's intra kernel sits in front of a prep kernel in a shared hardware queue)
@@ -890,8 +917,12 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
             HIP_TRY(hipEventCreateWithFlags(&ctx->join_ev[li], hipEventDisableTiming));
         }
         ps = ctx->aux[li];
-        HIP_TRY(hipEventRecord(ctx->fork_ev[li], s));
-        HIP_TRY(hipStreamWaitEvent(ps, ctx->fork_ev[li], 0));
+        if (early) {
+            HIP_TRY(hipStreamWaitEvent(ps, b->intra_done, 0));
+        } else {
+            HIP_TRY(hipEventRecord(ctx->fork_ev[li], s));
+            HIP_TRY(hipStreamWaitEvent(ps, ctx->fork_ev[li], 0));
+        }
     }
     if (prep) {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
@@ -902,30 +933,34 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], ps));
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
-        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
+        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT4]) {
-        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
+        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT8]) {
-        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
+        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT16]) {
-        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
+        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT32]) {
-        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
+        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_TSKIP]) {
-        residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, s>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
+        residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
     if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], 0));
+    if (rs != s) {
+        HIP_TRY(hipEventRecord(ctx->join2_ev[(size_t)b->lane], rs));
+        HIP_TRY(hipStreamWaitEvent(s, ctx->join2_ev[(size_t)b->lane], 0));
+    }
     if (b->dbk) {
         // deblocking edge / QpY map: depends on the records only
         dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);   // (context-size grid)
@@ -960,6 +995,10 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         ++tm.intra_launches;
     }
     HIP_TRY(hipGetLastError());
+    if (recon) {                                     // the residual pool and job lists are free again
+        if (!b->intra_done) HIP_TRY(hipEventCreateWithFlags(&b->intra_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(b->intra_done, s));
+    }
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
@@ -1100,8 +1139,10 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (ctx->pending == b) ctx->pending = nullptr;
-    // its lane may still run it: the allocation is reused by the next upload (another stream)
+    // its lane may still run it: the allocation is reused by the next upload (another stream); the
+    // lane stream's last run waited for every residual / prep kernel of the batch
     hipError_t e = b->stream ? hipStreamSynchronize(b->stream) : hipSuccess;
+    if (b->intra_done) (void)hipEventDestroy(b->intra_done);
     if (b->mem) {
         // keep the larger of (cache, this allocation) for the next upload (its runs are complete)
         if (!ctx->cache_mem || b->bytes > ctx->cache_bytes) {
@@ -1145,6 +1186,7 @@ int p265r_sync(p265r_ctx* ctx) {
     HIP_TRY(hipSetDevice(ctx->device));
     for (hipStream_t st : ctx->lanes) HIP_TRY(hipStreamSynchronize(st));
     for (hipStream_t st : ctx->aux) if (st) HIP_TRY(hipStreamSynchronize(st));
+    for (hipStream_t st : ctx->aux2) if (st) HIP_TRY(hipStreamSynchronize(st));
     ctx->lane_busy = 0;
     return P265R_OK;
 }

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/ab
 for rep in $(seq ${REPS:-2}); do
   for lib in ${LIBS:-default}; do
     if [ "$lib" = default ]; then path=$PWD/p265_amd/libp265r.so; else path=$PWD/p265_amd/libp265r_$lib.so; fi
-    P265R_LIB=$path timeout -k 10 200 python bench.py --experiment --no-cpu-baseline --no-e2e --no-verify ${BENCH_ARGS:-} > gpurun_out/ab/$lib.$rep.log 2>&1
+    P265R_LIB=$path timeout -k 10 150 python bench.py --experiment --no-cpu-baseline --no-e2e --no-verify ${BENCH_ARGS:-} > gpurun_out/ab/$lib.$rep.log 2>&1
     python3 -c "
 import json,sys
 d=json.loads(open('gpurun_out/ab/$lib.$rep.log').read().strip().splitlines()[-1])
