@@ -44,6 +44,9 @@ using namespace p265r;
 #ifndef P265R_EARLY_RESIDUAL
 #define P265R_EARLY_RESIDUAL 1     // re-runs: residual + prep start when the batch's previous intra phase ends
 #endif
+#ifndef P265R_PHASE_ORDER
+#define P265R_PHASE_ORDER 1        // pipelined contexts: one intra phase at a time; residual + prep overlap loop filters
+#endif
 #ifndef P265R_SPLIT_W16
 #define P265R_SPLIT_W16 1          // small split batches: W = 16 row kernel (0: the by-run W, A/B)
 #endif
@@ -150,6 +153,10 @@ struct p265r_ctx {
     std::vector<hipEvent_t> fork_ev, join_ev;
     std::vector<hipStream_t> aux2;    // aux2[i]: lane i's residual stream (early residual phase)
     std::vector<hipEvent_t> join2_ev;
+    // phase order of a pipelined context (P265R_PHASE_ORDER): the last intra launch and the last
+    // loop-filter launch of ANY lane, recorded on their lane streams
+    hipEvent_t last_intra_ev = nullptr, last_lf_ev = nullptr;
+    bool last_intra_valid = false, last_lf_valid = false;
     std::string describe;             // p265r_describe text
     unsigned char* dl_stage = nullptr;  // pinned download bounce buffer, 2 x kDlHalf (first download)
     hipEvent_t dl_ev[2] = {nullptr, nullptr};
@@ -535,6 +542,8 @@ void p265r_destroy(p265r_ctx* ctx) {
     for (hipStream_t st : ctx->aux) if (st) (void)hipStreamDestroy(st);
     for (hipStream_t st : ctx->aux2) if (st) (void)hipStreamDestroy(st);
     for (hipEvent_t e : ctx->join2_ev) if (e) (void)hipEventDestroy(e);
+    if (ctx->last_intra_ev) (void)hipEventDestroy(ctx->last_intra_ev);
+    if (ctx->last_lf_ev) (void)hipEventDestroy(ctx->last_lf_ev);
     for (hipEvent_t e : ctx->fork_ev) if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->join_ev) if (e) (void)hipEventDestroy(e);
     for (auto& r : ctx->runs) for (auto& e : r.ev) (void)hipEventDestroy(e);
@@ -886,9 +895,18 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // overwrite what the batch's intra phase reads (residual pool, job lists, job counts), so they
     // start as soon as the previous run's intra phase ends -- on two streams of the lane's own --
     // and overlap the previous run's loop filters instead of queueing behind them
-    const bool early = P265R_EARLY_RESIDUAL && prep && ctx->fork_prep == 1 && !ctx->timing && b->intra_done && !(skip & 1);
+    // phase order (pipelined contexts, no phase timing): the intra phases of different batches never
+    // overlap anything but the GPU's idle tail -- a batch's residual + prep phase waits for the last
+    // intra launch of ANY lane and then runs beside that batch's loop filters; its intra phase waits
+    // for the last loop-filter launch.  (Round 4: overlapping the intra kernel with the other phases
+    // cost as much as it hid -- pipelined 3 lanes = serial, 43.0 vs 43.5 M CTU/s -- because the row
+    // kernel holds the CUs' LDS and registers; residual / prep / SAO do not contend the same way.)
+    const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && ctx->fork_prep == 1 && !ctx->timing && !(skip & 1);
+    const bool early = !ordered && P265R_EARLY_RESIDUAL && prep && ctx->fork_prep == 1 && !ctx->timing && b->intra_done &&
+                       !(skip & 1);
+    hipEvent_t r_after = ordered ? (ctx->last_intra_valid ? ctx->last_intra_ev : nullptr) : (early ? b->intra_done : nullptr);
     hipStream_t rs = s;                              // the residual kernels' stream
-    if (early) {
+    if ((ordered || early) && r_after) {
         const size_t li = (size_t)b->lane;
         if (ctx->aux2.size() <= li) { ctx->aux2.resize(li + 1, nullptr); ctx->join2_ev.resize(li + 1, nullptr); }
         if (!ctx->aux2[li]) {
@@ -896,7 +914,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
             HIP_TRY(hipEventCreateWithFlags(&ctx->join2_ev[li], hipEventDisableTiming));
         }
         rs = ctx->aux2[li];
-        HIP_TRY(hipStreamWaitEvent(rs, b->intra_done, 0));
+        HIP_TRY(hipStreamWaitEvent(rs, r_after, 0));
     }
     if (prep && ctx->fork_prep) {
         // fork_prep 2: one prep stream shared by all lanes (fewer streams than HW queues, so no
@@ -917,8 +935,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
             HIP_TRY(hipEventCreateWithFlags(&ctx->join_ev[li], hipEventDisableTiming));
         }
         ps = ctx->aux[li];
-        if (early) {
-            HIP_TRY(hipStreamWaitEvent(ps, b->intra_done, 0));
+        if ((ordered || early) && r_after) {
+            HIP_TRY(hipStreamWaitEvent(ps, r_after, 0));
         } else {
             HIP_TRY(hipEventRecord(ctx->fork_ev[li], s));
             HIP_TRY(hipStreamWaitEvent(ps, ctx->fork_ev[li], 0));
@@ -974,9 +992,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         // per-CU workgroup slots cleared per run; the error word (d_err[0]) is sticky from upload on,
         // so p265r_batch_status / p265r_batch_download report a give-up in ANY run of the batch
         HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16, s));
+        if (ordered && ctx->last_lf_valid) HIP_TRY(hipStreamWaitEvent(s, ctx->last_lf_ev, 0));
         // does another lane have a run enqueued that the API has not synchronised since?  (host
         // state only, so the build a run gets is a function of the call sequence)
-        bool alone = (ctx->lane_busy & ~(1u << b->lane)) == 0u;
+        // (phase order: the intra phase has the GPU to itself by construction)
+        bool alone = ordered || (ctx->lane_busy & ~(1u << b->lane)) == 0u;
 #ifdef P265R_ALONE_PIPE
         alone = alone && ctx->pipeline == 1;       // A/B: a pipelined context never runs the W = 12 build
 #endif
@@ -998,6 +1018,9 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (recon) {                                     // the residual pool and job lists are free again
         if (!b->intra_done) HIP_TRY(hipEventCreateWithFlags(&b->intra_done, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(b->intra_done, s));
+        if (!ctx->last_intra_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->last_intra_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ctx->last_intra_ev, s));
+        ctx->last_intra_valid = true;
     }
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
@@ -1038,6 +1061,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         }
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
+    }
+    if (ordered) {                                   // the next batch's intra phase starts after this
+        if (!ctx->last_lf_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->last_lf_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ctx->last_lf_ev, s));
+        ctx->last_lf_valid = true;
     }
     if (ctx->timing) {
         HIP_TRY(hipEventRecord(ev[3], s));
