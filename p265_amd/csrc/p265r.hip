@@ -127,7 +127,11 @@ struct p265r_ctx {
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
                                // 45.5/44.9/44.4/44.7 M CTU/s; round 1, W=8: lead 0/1/2/3/5/8/17 ->
                                // 10.40/10.10/10.40/10.09/10.07/10.35/10.38 ms)
-    bool stream_prio = false;  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
+    bool stream_prio = false;
+    // occupancy caps by dynamic-LDS padding of the SAO / residual launches (P265R_SAO_LDS /
+    // P265R_RES_LDS bytes per block, experiments builds): fewer waves per CU streamed faster in the
+    // HBM probe (tools/bw_probe.hip)
+    int sao_lds = 0, res_lds = 0;  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
     int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (experiments:
                                // P265R_PIPE_WAVES 4, 6, 8)
     int num_cus = 256;
@@ -504,6 +508,10 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
         if (w == 4 || w == 6 || w == 8) ctx->pipe_waves = w;
     }
     if (const char* v = std::getenv("P265R_STREAM_PRIO")) ctx->stream_prio = std::atoi(v) != 0;
+    for (const char* k : {"P265R_SAO_LDS", "P265R_RES_LDS"})
+        if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
+    if (const char* v = std::getenv("P265R_SAO_LDS")) ctx->sao_lds = std::min(65536, std::max(0, std::atoi(v)));
+    if (const char* v = std::getenv("P265R_RES_LDS")) ctx->res_lds = std::min(32768, std::max(0, std::atoi(v)));
 #endif
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -901,8 +909,16 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // for the last loop-filter launch.  (Round 4: overlapping the intra kernel with the other phases
     // cost as much as it hid -- pipelined 3 lanes = serial, 43.0 vs 43.5 M CTU/s -- because the row
     // kernel holds the CUs' LDS and registers; residual / prep / SAO do not contend the same way.)
-    const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && ctx->fork_prep == 1 && !ctx->timing && !(skip & 1);
-    const bool early = !ordered && P265R_EARLY_RESIDUAL && prep && ctx->fork_prep == 1 && !ctx->timing && b->intra_done &&
+    // (only batches whose intra launch fills the chip -- a workgroup per CU at least: the launches of
+    // small batches (tile units, decoder batches) occupy a few CUs each and SHOULD run side by side)
+    // A batch smaller than the chip (tile units, decoder batches: a few workgroups per launch) keeps
+    // every phase on its lane stream: the extra prep / residual streams would outnumber the hardware
+    // queues (4 by default) and put one lane's kernels behind another's -- C5 with 4 lanes: 2.3 M CTU/s
+    // forked vs 3.0 M unforked, 5.2 M unforked with GPU_MAX_HW_QUEUES=8 (round 4, tools/ab_env2.sh)
+    const bool big = b->n_pics >= ctx->num_cus;
+    const int fork_prep = big ? ctx->fork_prep : 0;
+    const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && fork_prep == 1 && !ctx->timing && !(skip & 1);
+    const bool early = !ordered && P265R_EARLY_RESIDUAL && prep && fork_prep == 1 && !ctx->timing && b->intra_done &&
                        !(skip & 1);
     hipEvent_t r_after = ordered ? (ctx->last_intra_valid ? ctx->last_intra_ev : nullptr) : (early ? b->intra_done : nullptr);
     hipStream_t rs = s;                              // the residual kernels' stream
@@ -916,10 +932,10 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         rs = ctx->aux2[li];
         HIP_TRY(hipStreamWaitEvent(rs, r_after, 0));
     }
-    if (prep && ctx->fork_prep) {
+    if (prep && fork_prep) {
         // fork_prep 2: one prep stream shared by all lanes (fewer streams than HW queues, so no
         // lane's intra kernel sits in front of a prep kernel in a shared hardware queue)
-        const size_t li = ctx->fork_prep == 2 ? 0 : (size_t)b->lane;
+        const size_t li = fork_prep == 2 ? 0 : (size_t)b->lane;
         if (ctx->aux.size() <= li) {
             ctx->aux.resize(li + 1, nullptr); ctx->fork_ev.resize(li + 1, nullptr); ctx->join_ev.resize(li + 1, nullptr);
         }
@@ -948,33 +964,33 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         // waves start before the residual kernels fill the chip
         intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, 0, ps>>>(b->d_pics, g, b->view);
         ++tm.residual_launches;
-        if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], ps));
+        if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[fork_prep == 2 ? 0 : (size_t)b->lane], ps));
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
-        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
+        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT4]) {
-        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
+        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT8]) {
-        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
+        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT16]) {
-        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
+        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_DCT32]) {
-        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
+        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
         ++tm.residual_launches;
     }
     if (recon && !(skip & 1) && b->n_jobs[RC_TSKIP]) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
-    if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[ctx->fork_prep == 2 ? 0 : (size_t)b->lane], 0));
+    if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[fork_prep == 2 ? 0 : (size_t)b->lane], 0));
     if (rs != s) {
         HIP_TRY(hipEventRecord(ctx->join2_ev[(size_t)b->lane], rs));
         HIP_TRY(hipStreamWaitEvent(s, ctx->join2_ev[(size_t)b->lane], 0));
@@ -1033,8 +1049,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         const long long waves = (long long)sao16_units(g) * b->n_pics;
         if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
         const unsigned blocks = (unsigned)((waves + 3) / 4 + 7) / 8 * 8;
-        if (g.ctb_log2 == 6) sao_strip16_kernel<6><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
-        else sao_strip16_kernel<5><<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
+        if (g.ctb_log2 == 6) sao_strip16_kernel<6><<<blocks, 256, ctx->sao_lds, s>>>(b->d_pics, g, b->view, b->n_pics);
+        else sao_strip16_kernel<5><<<blocks, 256, ctx->sao_lds, s>>>(b->d_pics, g, b->view, b->n_pics);
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
     } else if (b->sao && !b->dbk && ctx->sao_rows && !(skip & 4)) {
