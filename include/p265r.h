@@ -184,8 +184,12 @@ int  p265r_wait(p265r_ctx* ctx);
 /* Block until the context's streams are idle. */
 int  p265r_sync(p265r_ctx* ctx);
 /* Batch pipelining (no counterpart in the reference; a throughput knob of this back-end):
- * batches uploaded afterwards are bound round-robin to `depth` (1..4) HIP streams, so the
- * residual and loop-filter phases of one batch run beside the intra phase of another.
+ * batches uploaded afterwards are bound round-robin to `depth` (1..8) HIP streams, so the
+ * residual and loop-filter phases of one batch run beside the intra phase of another (small
+ * batches: whole batches side by side).  Every stream wants a hardware queue of its own: HIP's
+ * default GPU_MAX_HW_QUEUES=4 serves depth <= 3 (+ the upload stream); set GPU_MAX_HW_QUEUES >=
+ * depth + 1 before the process first touches HIP for deeper pipelines (2 x depth + 2 for batches of
+ * >= one picture per CU, whose prep / residual phases get streams of their own).
  * Runs of one batch stay ordered; p265r_sync waits for every stream.  Default 1. */
 int  p265r_set_pipeline(p265r_ctx* ctx, int depth);
 /* Enable (1, which also starts a new accumulation) / disable (0) per-phase HIP-event

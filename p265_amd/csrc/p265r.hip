@@ -1236,7 +1236,7 @@ int p265r_sync(p265r_ctx* ctx) {
 }
 
 int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
-    if (!ctx || depth < 1 || depth > 4) return P265R_EINVAL;
+    if (!ctx || depth < 1 || depth > 8) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     while ((int)ctx->lanes.size() < depth) {
         hipStream_t st = nullptr;
