@@ -368,9 +368,16 @@ def main():
     # one hardware queue per stream (the lanes + the upload stream): HIP's default 4 would put two C5
     # lanes behind each other (c5, 8 lanes: 3.0 M CTU/s at 4 queues, 8.4 M at 12; c3 measured best
     # at the default: 43.4 vs 41.8 M at 8 queues -- its prep / residual streams then interleave).
-    # Set before this process first touches HIP (dist.init below); an explicit setting wins.
+    # Raised (never lowered) before this process first touches HIP (dist.init below); the GPU boxes
+    # export the default 4 explicitly.
     if a.workload == "c5":
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(32, a.pipeline + 4)))
+        want = min(32, a.pipeline + 4)
+        try:
+            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        except ValueError:
+            have = 4
+        if have < want:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     exp = experiment_env()
     if exp and not a.experiment:
         sys.stderr.write("bench.py: refusing to run with library experiment knobs set: %s "
