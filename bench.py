@@ -293,7 +293,7 @@ def end_to_end(device, reps=16, threads=16):
     n_ctu = sum(len(p.picture.ctus) for p in pics)
     decoder.decode_bytes(one, device=device, threads=threads)      # warm (contexts, kernels)
     runs = []
-    for _ in range(3):
+    for _ in range(5):                     # best of 5: a 0.1-s host-bound run is noisy on a shared host
         t0 = time.perf_counter()
         frames = decoder.decode_bytes(data, device=device, threads=threads)
         runs.append(time.perf_counter() - t0)
