@@ -917,7 +917,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // forked vs 3.0 M unforked, 5.2 M unforked with GPU_MAX_HW_QUEUES=8 (round 4, tools/ab_env2.sh)
     const bool big = b->n_pics >= ctx->num_cus;
     const int fork_prep = big ? ctx->fork_prep : 0;
-    const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && fork_prep == 1 && !ctx->timing && !(skip & 1);
+    const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && fork_prep == 1 && !ctx->timing;
     const bool early = !ordered && P265R_EARLY_RESIDUAL && prep && fork_prep == 1 && !ctx->timing && b->intra_done &&
                        !(skip & 1);
     hipEvent_t r_after = ordered ? (ctx->last_intra_valid ? ctx->last_intra_ev : nullptr) : (early ? b->intra_done : nullptr);

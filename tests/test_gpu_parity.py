@@ -217,6 +217,57 @@ def test_pipelined_batches(recon_mod, sync_first):
                 np.testing.assert_array_equal(outs[k][i][c], ref[c], err_msg="set %d pic %d c%d" % (k, i, c))
 
 
+def test_pipelined_small_batches_eight_lanes(recon_mod):
+    """p265r_set_pipeline(8): eight small batches (every phase on its lane stream), runs
+    interleaved over the lanes twice, then downloaded in reverse order: every output equals
+    the oracle."""
+    params = R.make_params(pic_width=192, pic_height=128)
+    sets = [[synth.make_picture(params, 900 + 10 * k + s, perf=bool((k + s) % 2)) for s in range(2)] for k in range(8)]
+    pd = R.params_dict(params)
+    with recon_mod.ReconContext(params) as ctx:
+        ctx.set_pipeline(8)
+        bs = [ctx.upload(p) for p in sets]
+        for _ in range(2):
+            for b in bs:
+                ctx.run(b)
+        outs = [ctx.download(b) for b in reversed(bs)][::-1]
+        for b in bs:
+            b.free()
+    for k, pics in enumerate(sets):
+        for i, p in enumerate(pics):
+            ref = O.decode_picture(pd, p.as_oracle_dict())[1]
+            for c in range(3):
+                np.testing.assert_array_equal(outs[k][i][c], ref[c], err_msg="set %d pic %d c%d" % (k, i, c))
+
+
+def test_pipelined_chip_filling_batches_phase_order(recon_mod):
+    """Batches of at least one picture per CU take the phase-ordered path (forked prep and
+    residual streams, one intra launch at a time, the next batch's residual phase beside the
+    previous one's loop filters): three such batches of 64x64 pictures, each run twice,
+    interleaved; the first, a middle and the last picture of every batch equal the oracle."""
+    params = R.make_params(pic_width=64, pic_height=64)
+    distinct = [synth.make_picture(params, 950 + s, perf=bool(s % 2)) for s in range(4)]
+    pd = R.params_dict(params)
+    ref = [O.decode_picture(pd, p.as_oracle_dict())[1] for p in distinct]
+    with recon_mod.ReconContext(params) as ctx:
+        n = int(ctx.describe()["num_cus"])               # one picture per CU: the large-batch path
+        sets = [[distinct[(k + i) % 4] for i in range(n)] for k in range(3)]
+        ctx.set_pipeline(3)
+        bs = [ctx.upload(p) for p in sets]
+        for _ in range(2):
+            for b in bs:
+                ctx.run(b)
+        ctx.sync()
+        for k, b in enumerate(bs):
+            ctx.status(b)
+            idx = [0, n // 2, n - 1]
+            outs = ctx.download(b, only=idx)
+            for i in idx:
+                for c in range(3):
+                    np.testing.assert_array_equal(outs[i][c], ref[(k + i) % 4][c], err_msg="batch %d pic %d c%d" % (k, i, c))
+            b.free()
+
+
 @pytest.mark.parametrize("ctb_log2,deblocking", [(6, False), (5, False), (4, False), (6, "random"), (5, True)])
 def test_ragged_batch(recon_mod, schedule, ctb_log2, deblocking):
     """Pictures of different sizes in ONE batch (p265r_picture.pic_width / pic_height, up to the
