@@ -272,7 +272,7 @@ def exit_code(out):
     return 3 if v is not None and not v.get("ok") else 0
 
 
-def end_to_end(device, reps=16, threads=16):
+def end_to_end(device, reps=32, threads=16):
     """Bitstream bytes -> decoded planes in host memory, from a real (synthetic) 1080p stream.
 
     tests/golden/synth_1080p_4pic.bin (4 IDR pictures with MD5 picture-hash SEI, made by

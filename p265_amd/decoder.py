@@ -154,8 +154,10 @@ class _Lane:
         self.key, self.ctx, self.lock = key, ctx, threading.Lock()
 
 
-# end-to-end defaults (tools/e2e_profile.py sweep on the GPU box, 64 x 1080p, 16 host threads)
-DEFAULT_BATCH, DEFAULT_DEPTH, DEFAULT_CHUNK = 8, 2, 1 << 20
+# end-to-end defaults (tools/e2e_profile.py sweep on the GPU box, 128 x 1080p, 16 host threads; round 4,
+# after small batches stopped forking their own streams: 8-picture batches over 4 lanes 504 k CTU/s,
+# over 2 lanes 354 k)
+DEFAULT_BATCH, DEFAULT_DEPTH, DEFAULT_CHUNK = 8, 4, 1 << 20
 
 
 def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT_BATCH, threads: int = 0,
