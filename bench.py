@@ -104,7 +104,7 @@ def issue_rates(workload, kernel_prefix, avg_ms):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default c3: 30, c5: 64 -- 16 lanes to fill)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=("c3", "c5"), default="c3")
     ap.add_argument("--frames", type=int, default=512, help="c3: 1080p pictures per GPU per step")
@@ -112,8 +112,8 @@ def parse():
     ap.add_argument("--c5-frames", type=int, default=2, help="c5: 4K frames per step (x4 tile units, all ranks)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="resident batches run round-robin on this many HIP streams (p265r_set_pipeline; default "
-                         "c3: 3 -- one batch's residual + prep phase beside another's loop filters; c5: 8 -- the "
-                         "8-unit batches fill a few CUs each, so whole batches run side by side)")
+                         "c3: 3 -- one batch's residual + prep phase beside another's loop filters; c5: 16 -- an "
+                         "8-unit batch fills 16 CUs, so 16 whole batches run side by side)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the bitstream -> planes end-to-end leg")
@@ -368,9 +368,12 @@ def build_workload(a, rank, world):
 def main():
     a = parse()
     if a.pipeline is None:
-        a.pipeline = 8 if a.workload == "c5" else 3
+        a.pipeline = 16 if a.workload == "c5" else 3
+    if a.steps is None:
+        a.steps = 64 if a.workload == "c5" else 30
     # one hardware queue per stream (the lanes + the upload stream): HIP's default 4 would put two C5
-    # lanes behind each other (c5, 8 lanes: 3.0 M CTU/s at 4 queues, 8.4 M at 12; c3 measured best
+    # lanes behind each other (c5, 8 lanes: 3.0 M CTU/s at 4 queues, 8.4 M at 12; 16 lanes at 20 queues:
+    # 16.4 M, every CU holding one unit's workgroup; c3 measured best
     # at the default: 43.4 vs 41.8 M at 8 queues -- its prep / residual streams then interleave).
     # Raised (never lowered) before this process first touches HIP (dist.init below); the GPU boxes
     # export the default 4 explicitly.

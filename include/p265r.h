@@ -184,7 +184,7 @@ int  p265r_wait(p265r_ctx* ctx);
 /* Block until the context's streams are idle. */
 int  p265r_sync(p265r_ctx* ctx);
 /* Batch pipelining (no counterpart in the reference; a throughput knob of this back-end):
- * batches uploaded afterwards are bound round-robin to `depth` (1..8) HIP streams, so the
+ * batches uploaded afterwards are bound round-robin to `depth` (1..16) HIP streams, so the
  * residual and loop-filter phases of one batch run beside the intra phase of another (small
  * batches: whole batches side by side).  Every stream wants a hardware queue of its own: HIP's
  * default GPU_MAX_HW_QUEUES=4 serves depth <= 3 (+ the upload stream); set GPU_MAX_HW_QUEUES >=

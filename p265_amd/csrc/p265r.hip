@@ -131,7 +131,8 @@ struct p265r_ctx {
     // occupancy caps by dynamic-LDS padding of the SAO / residual launches (P265R_SAO_LDS /
     // P265R_RES_LDS bytes per block, experiments builds): fewer waves per CU streamed faster in the
     // HBM probe (tools/bw_probe.hip)
-    int sao_lds = 0, res_lds = 0;  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
+    int sao_lds = 0, res_lds = 0;
+    int order_r = 1;               // P265R_ORDER_R=0 (experiments): ordered runs' residual phase waits only for its own batch  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
     int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (experiments:
                                // P265R_PIPE_WAVES 4, 6, 8)
     int num_cus = 256;
@@ -510,6 +511,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_STREAM_PRIO")) ctx->stream_prio = std::atoi(v) != 0;
     for (const char* k : {"P265R_SAO_LDS", "P265R_RES_LDS"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
+    if (const char* v = std::getenv("P265R_ORDER_R")) ctx->order_r = std::atoi(v) != 0;
     if (const char* v = std::getenv("P265R_SAO_LDS")) ctx->sao_lds = std::min(65536, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("P265R_RES_LDS")) ctx->res_lds = std::min(32768, std::max(0, std::atoi(v)));
 #endif
@@ -921,6 +923,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     const bool early = !ordered && P265R_EARLY_RESIDUAL && prep && fork_prep == 1 && !ctx->timing && b->intra_done &&
                        !(skip & 1);
     hipEvent_t r_after = ordered ? (ctx->last_intra_valid ? ctx->last_intra_ev : nullptr) : (early ? b->intra_done : nullptr);
+    if (ordered && ctx->order_r == 0) r_after = b->intra_done;     // (A/B: residual phase not held back)
     hipStream_t rs = s;                              // the residual kernels' stream
     if ((ordered || early) && r_after) {
         const size_t li = (size_t)b->lane;
@@ -1236,7 +1239,7 @@ int p265r_sync(p265r_ctx* ctx) {
 }
 
 int p265r_set_pipeline(p265r_ctx* ctx, int depth) {
-    if (!ctx || depth < 1 || depth > 8) return P265R_EINVAL;
+    if (!ctx || depth < 1 || depth > 16) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     while ((int)ctx->lanes.size() < depth) {
         hipStream_t st = nullptr;

@@ -107,7 +107,7 @@ def _context(params, device, pipeline):
         ctx = idle.pop() if idle else None         # checked out: one user at a time
     if ctx is None:
         ctx = recon.ReconContext(params, device=device)
-        ctx.set_pipeline(max(1, min(8, pipeline)))
+        ctx.set_pipeline(max(1, min(16, pipeline)))
     return key, ctx
 
 
