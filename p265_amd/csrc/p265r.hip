@@ -1265,11 +1265,13 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
-        "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, "
+        "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"phase_order\": %d, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
-        ctx->row_waves ? "fixed" : "W=12 (6 per SIMD) while no other lane has a run enqueued since the API synchronised "
-                                   "it, else pipe_waves",
+        ctx->row_waves ? "fixed" : "batches of >= 1 picture per CU in a pipelined context: W=12, one intra launch at a time "
+                                   "(phase order); small batches (< 1 picture per CU: component split, W=16): side by side; "
+                                   "otherwise W=12 while no other lane has a run enqueued since the API synchronised it, "
+                                   "else pipe_waves",
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
         ctx->pipeline, ctx->fork_prep, ctx->pipe_waves, hwq_env(), ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG
@@ -1277,7 +1279,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
 #else
         0,
 #endif
-        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0,
+        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, P265R_PHASE_ORDER,
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;
     if (size > 0) {
