@@ -901,22 +901,19 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     ctx->lane_busy |= 1u << b->lane;
     const bool prep = recon && ctx->schedule == 1 && !(skip & 2);
     hipStream_t ps = s;                              // the prep kernel's stream
-    // early residual phase (re-runs, no phase timing): the residual kernels and the job prep only
-    // overwrite what the batch's intra phase reads (residual pool, job lists, job counts), so they
-    // start as soon as the previous run's intra phase ends -- on two streams of the lane's own --
-    // and overlap the previous run's loop filters instead of queueing behind them
-    // phase order (pipelined contexts, no phase timing): the intra phases of different batches never
-    // overlap anything but the GPU's idle tail -- a batch's residual + prep phase waits for the last
-    // intra launch of ANY lane and then runs beside that batch's loop filters; its intra phase waits
-    // for the last loop-filter launch.  (Round 4: overlapping the intra kernel with the other phases
-    // cost as much as it hid -- pipelined 3 lanes = serial, 43.0 vs 43.5 M CTU/s -- because the row
-    // kernel holds the CUs' LDS and registers; residual / prep / SAO do not contend the same way.)
-    // (only batches whose intra launch fills the chip -- a workgroup per CU at least: the launches of
-    // small batches (tile units, decoder batches) occupy a few CUs each and SHOULD run side by side)
-    // A batch smaller than the chip (tile units, decoder batches: a few workgroups per launch) keeps
-    // every phase on its lane stream: the extra prep / residual streams would outnumber the hardware
-    // queues (4 by default) and put one lane's kernels behind another's -- C5 with 4 lanes: 2.3 M CTU/s
-    // forked vs 3.0 M unforked, 5.2 M unforked with GPU_MAX_HW_QUEUES=8 (round 4, tools/ab_env2.sh)
+    // Stream plan of one run (no phase timing):
+    // * a batch smaller than the chip (< 1 picture per CU: tile units, decoder batches, a few workgroups
+    //   per launch) keeps every phase on its lane stream, and such batches run side by side: extra prep /
+    //   residual streams would outnumber the hardware queues (4 by default) and put one lane's kernels
+    //   behind another's (C5, 4 lanes: 2.3 M CTU/s forked vs 3.0 M unforked; 5.2 M unforked at
+    //   GPU_MAX_HW_QUEUES=8, round 4);
+    // * a chip-filling batch in a pipelined context runs in PHASE ORDER: its residual + prep phase (on
+    //   two streams of the lane's own) waits for the last intra launch of ANY lane and runs beside the
+    //   previous batch's loop filters; its intra phase waits for the last loop-filter launch, so the row
+    //   kernel (W = 12, all of every CU's registers) always runs alone -- overlapping it with the other
+    //   phases cost as much as it hid (3 lanes unordered = serial, 43.0 vs 43.5 M CTU/s, round 4);
+    // * otherwise (a lone lane's re-runs) the EARLY residual phase: residual + prep start when this
+    //   batch's previous intra phase ends, beside its previous loop filters.
     const bool big = b->n_pics >= ctx->num_cus;
     const int fork_prep = big ? ctx->fork_prep : 0;
     const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && fork_prep == 1 && !ctx->timing;
