@@ -219,51 +219,54 @@ def sha_planes(planes):
     return hashlib.sha256(b"".join(np.ascontiguousarray(p).tobytes() for p in planes)).hexdigest()
 
 
-def verify_planes(params, pics, got, threads):
-    """Compare downloaded planes with the C oracle (oracle/recon_oracle.c, the checker).
-
-    ``got``: {picture index: [Y, Cb, Cr]} for pictures of ``pics``; identical Picture objects
-    (the replicated synthetic pictures) are decoded once.  -> (n_checked, [mismatching indices])."""
-    from oracle import c_oracle
-    distinct = {}
-    for i in got:
-        distinct.setdefault(id(pics[i]), pics[i])
-    keys = list(distinct)
-    ref = c_oracle.decode(params, [distinct[k] for k in keys], threads=threads, with_recon=False)
-    want = {k: sha_planes(r[1]) for k, r in zip(keys, ref)}
-    bad = [i for i, planes in sorted(got.items()) if sha_planes(planes) != want[id(pics[i])]]
-    return len(got), bad
+def digest_mismatches(pics, want, got):
+    """Indices of the pictures whose device digests ``got`` ([n, 3] uint64, p265r_batch_digest)
+    differ from the oracle's ``want`` ({id(picture): 3 digests})."""
+    return [i for i, p in enumerate(pics) if not np.array_equal(got[i], want[id(p)])]
 
 
 def verify(ctxs, groups, a, threads, ran=None):
-    """After the timed region: every resident batch's error word (p265r_batch_status: a row-kernel
-    dependency give-up in ANY of its runs) and the planes of pictures_to_check() of every batch that
-    ran (``ran``: batch slots; with fewer steps than pipeline lanes some never do), against the C
-    oracle.  -> the line's "verified" object."""
-    from p265_amd import _lib
+    """After the timed region: EVERY picture of every resident batch that ran (``ran``: batch slots;
+    with fewer steps than pipeline lanes some never do) through its device digest (p265r_batch_digest,
+    which also reports the sticky row-kernel error word: a dependency give-up in ANY run) against the
+    digest of the C oracle's decode of the same records; and, as a check of the digest itself, the
+    downloaded planes of each batch's first and last pictures (SHA-256 and host digest).
+    -> the line's "verified" object."""
+    from p265_amd import _lib, digest
+    from oracle import c_oracle
     n_checked, bad, status_ok, distinct = 0, [], True, set()
     for (ctx, batches), (params, gp) in zip(ctxs, groups):
+        uniq = {}
+        for p in gp:
+            uniq.setdefault(id(p), p)
+        keys = list(uniq)
+        ref = c_oracle.decode(params, [uniq[k] for k in keys], threads=threads, with_recon=False)
+        want = {k: digest.picture_digest(r[1]) for k, r in zip(keys, ref)}
+        want_sha = {k: sha_planes(r[1]) for k, r in zip(keys, ref)}
+        distinct |= set(keys)
         idx = pictures_to_check(len(gp), a.unique if a.workload == "c3" else len(gp))
-        distinct |= {id(gp[i]) for i in idx}
         for bi, b in enumerate(batches):
             if ran is not None and bi not in ran:
                 continue
             try:
-                ctx.status(b)
+                got = ctx.digest(b)
             except _lib.P265RError as e:
                 status_ok = False
                 bad.append("batch %d: %s" % (bi, e))
                 continue
+            n_checked += len(gp)
+            bad += ["batch %d picture %d" % (bi, i) for i in digest_mismatches(gp, want, got)]
             outs = ctx.download(b, only=idx)
-            n, mism = verify_planes(params, gp, {i: outs[i] for i in idx}, threads)
-            n_checked += n
-            bad += ["batch %d picture %d" % (bi, i) for i in mism]
+            for i in idx:
+                if sha_planes(outs[i]) != want_sha[id(gp[i])] or not np.array_equal(digest.picture_digest(outs[i]), got[i]):
+                    bad.append("batch %d picture %d (download)" % (bi, i))
     return {"ok": status_ok and not bad, "pictures": n_checked, "distinct": len(distinct),
             "batches": sum(1 for _, bs in ctxs for bi in range(len(bs)) if ran is None or bi in ran),
             "status_ok": status_ok, "mismatches": bad[:8],
-            "how": "after the timed runs: p265r_batch_status (sticky row-kernel error word) of every resident "
-                   "batch, then the decoded planes of its first and last pictures (SHA-256) against "
-                   "oracle/recon_oracle.c on the same records"}
+            "how": "after the timed runs: p265r_batch_digest (device digest of every picture's three output planes, "
+                   "plus the sticky row-kernel error word) of every resident batch that ran, against the digests of "
+                   "oracle/recon_oracle.c's decode of the same records; each batch's first and last pictures are "
+                   "also downloaded and compared by SHA-256 and host digest (p265_amd/digest.py)"}
 
 
 def exit_code(out):

@@ -116,7 +116,8 @@ int  p265fe_take(p265fe_decoder* dec, p265fe_pictures** out);
  * chunk overlaps the slowest pictures of the previous one; p265fe_feed returns the number of
  * pictures submitted and not yet taken.  p265fe_take then hands out the PARSED PREFIX in decode
  * order (possibly empty; a picture that failed to parse ends the prefix and its error code is
- * returned once the pictures before it are taken).  p265fe_wait blocks until the next picture in
+ * returned once the pictures before it are taken -- that take reports it once and drops the failed
+ * picture, so the next take continues with the pictures after it).  p265fe_wait blocks until the next picture in
  * decode order is parsed (all = 0) or every submitted one is (all = 1), and returns how many are
  * ready to take. */
 int  p265fe_wait(p265fe_decoder* dec, int all);

@@ -174,6 +174,14 @@ int  p265r_batch_download(p265r_ctx* ctx, p265r_batch* batch, const p265r_pictur
  * says which).  Lets a caller that re-runs a resident batch (a benchmark) check the work it
  * timed without downloading it.  No counterpart in the reference (which cannot fail this way). */
 int  p265r_batch_status(p265r_ctx* ctx, p265r_batch* batch);
+/* Per-picture digest of a batch's planes after every run enqueued on it, computed on the device
+ * (no plane download): which = 0 the decoded (output) planes, 1 the reconstruction before the
+ * in-loop filters.  out[3 * i + c] = sum over the 4-sample words of plane c of picture i (row y,
+ * word k; the picture's own width W, W/4 words per row) of mix64(word | (y * W/4 + k) << 32)
+ * mod 2^64, mix64 = the splitmix64 finalizer (p265_amd/digest.py restates it on the host);
+ * n = 3 * the batch's pictures.  Returns what p265r_batch_status returns afterwards.  Lets a
+ * benchmark check every picture it timed.  No counterpart in the reference. */
+int  p265r_batch_digest(p265r_ctx* ctx, p265r_batch* batch, int which, uint64_t* out, int n);
 int  p265r_batch_free(p265r_ctx* ctx, p265r_batch* batch);
 
 /* Convenience: upload + run (asynchronous) ... */
@@ -188,8 +196,9 @@ int  p265r_sync(p265r_ctx* ctx);
  * residual and loop-filter phases of one batch run beside the intra phase of another (small
  * batches: whole batches side by side).  Every stream wants a hardware queue of its own: HIP's
  * default GPU_MAX_HW_QUEUES=4 serves depth <= 3 (+ the upload stream); set GPU_MAX_HW_QUEUES >=
- * depth + 1 before the process first touches HIP for deeper pipelines (2 x depth + 2 for batches of
- * >= one picture per CU, whose prep / residual phases get streams of their own).
+ * depth + 1 before the process first touches HIP for deeper pipelines (min(32, 2 x depth + 2) for
+ * batches of >= one picture per CU, whose prep / residual phases get streams of their own; the
+ * runtime accepts at most 32, so past depth 15 such batches share hardware queues).
  * Runs of one batch stay ordered; p265r_sync waits for every stream.  Default 1. */
 int  p265r_set_pipeline(p265r_ctx* ctx, int depth);
 /* Enable (1, which also starts a new accumulation) / disable (0) per-phase HIP-event

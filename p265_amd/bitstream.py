@@ -280,6 +280,9 @@ class StreamParser:
         cnt = lib.p265fe_take(self.h, ctypes.byref(sp))
         if cnt < 0:
             if cnt in (EBITSTREAM, EUNSUPPORTED):
+                if self.asynchronous:       # the failed picture is reported once and dropped (p265fe.h)
+                    self.pending = max(0, self.pending - 1)
+                    self.n_pictures += 1
                 _fail(lib, self.h, cnt, "p265fe_take")
             raise MemoryError("p265fe_take failed (%d)" % cnt)
         owner = _SetOwner(lib, sp)

@@ -1,0 +1,55 @@
+// Per-picture digest of the decoded planes (p265r_batch_digest): lets a caller that re-runs a
+// resident batch (bench.py) check EVERY picture it timed against the oracle without downloading
+// the planes.  No counterpart in the reference (its planes are never produced, cu.py:487-488).
+//
+// digest(plane) = sum over the plane's 4-sample words (row y, word i; W/4 words per row, the
+// picture's own width) of mix64(word | (y * W/4 + i) << 32) mod 2^64, mix64 = the splitmix64
+// finalizer.  Position-keyed and order-free, so the partial sums of any split of the plane add up;
+// p265_amd/digest.py restates it with numpy for the host side.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "intra.h"
+
+namespace p265r {
+
+__device__ __forceinline__ uint64_t digest_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+constexpr int kDigestRows = 8;     // plane rows per workgroup
+
+// grid (ceil(max plane height / kDigestRows), 3 planes, pictures), 256 threads; out[3 * pic + c]
+// must be zero on entry (partial sums are added atomically, one per wave)
+__global__ __launch_bounds__(256) void digest_kernel(const DevPic* __restrict__ pics, Geo g, int use_out,
+                                                     unsigned long long* __restrict__ out) {
+    const int c = blockIdx.y, pic = blockIdx.z;
+    const DevPic& P = pics[pic];
+    const uint32_t wh = P.wh;
+    const int sub = c ? 1 : 0;
+    const int w = (int)(wh & 0xffffu) >> sub, h = (int)(wh >> 16) >> sub;
+    const int y0 = blockIdx.x * kDigestRows;
+    if (y0 >= h) return;                                 // (block-uniform)
+    const int rows = min(kDigestRows, h - y0);
+    const int wpr = w >> 2;                              // words per row (widths are multiples of 4)
+    const uint8_t* plane = use_out ? P.out[c] : P.rec[c];
+    const int stride = g.stride[c];
+    uint64_t acc = 0;
+    for (int e = threadIdx.x; e < rows * wpr; e += 256) {
+        const int yy = e / wpr, i = e - yy * wpr;
+        const int y = y0 + yy;
+        const uint32_t word = *reinterpret_cast<const uint32_t*>(plane + (size_t)y * stride + 4 * i);
+        acc += digest_mix64((uint64_t)word | (uint64_t)((uint32_t)(y * wpr + i)) << 32);
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)acc, s, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), s, 64);
+        acc += (uint64_t)lo | (uint64_t)hi << 32;
+    }
+    if ((threadIdx.x & 63) == 0) atomicAdd(out + 3 * pic + c, (unsigned long long)acc);
+}
+
+}  // namespace p265r

@@ -470,7 +470,15 @@ int p265fe_take(p265fe_decoder* d, p265fe_pictures** out) {
         for (size_t i = 0; i < k; ++i) a.slots.pop_front();
         a.base += k;
         a.next_work -= k;
-        if (code && set->jobs.empty()) { delete set; return code; }
+        if (code && set->jobs.empty()) {
+            // the failed picture is reported ONCE and dropped: later takes hand out the pictures
+            // after it (a caller resyncs at the next IRAP), and feed's pending count drains
+            a.slots.pop_front();
+            a.base += 1;
+            a.next_work -= 1;
+            delete set;
+            return code;
+        }
         *out = set;
         return (int)set->jobs.size();
     }

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/p265r.h"
+#include "digest.h"
 #include "intra.h"
 #include "intra_prep.h"
 #include "intra_rows.h"
@@ -931,6 +932,10 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         }
         rs = ctx->aux2[li];
         HIP_TRY(hipStreamWaitEvent(rs, r_after, 0));
+        // the batch's own previous intra phase (the last reader of its residual pool and job lists):
+        // r_after is the last intra launch of ANY lane, which only orders after it when every intra
+        // launch of the context ran phase-ordered (a small or timed batch on another lane does not)
+        if (b->intra_done && r_after != b->intra_done) HIP_TRY(hipStreamWaitEvent(rs, b->intra_done, 0));
     }
     if (prep && fork_prep) {
         // fork_prep 2: one prep stream shared by all lanes (fewer streams than HW queues, so no
@@ -953,6 +958,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         ps = ctx->aux[li];
         if ((ordered || early) && r_after) {
             HIP_TRY(hipStreamWaitEvent(ps, r_after, 0));
+            if (b->intra_done && r_after != b->intra_done) HIP_TRY(hipStreamWaitEvent(ps, b->intra_done, 0));
         } else {
             HIP_TRY(hipEventRecord(ctx->fork_ev[li], s));
             HIP_TRY(hipStreamWaitEvent(ps, ctx->fork_ev[li], 0));
@@ -1177,6 +1183,25 @@ int p265r_batch_status(p265r_ctx* ctx, p265r_batch* b) {
         return P265R_EHIP;
     }
     return P265R_OK;
+}
+
+int p265r_batch_digest(p265r_ctx* ctx, p265r_batch* b, int which, uint64_t* out, int n) {
+    if (!ctx || !b || !out || n != 3 * b->n_pics || (which != 0 && which != 1)) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    // after every run enqueued on the batch's lane (stream order); one device buffer per call
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), sizeof(uint64_t) * (size_t)n));
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(uint64_t) * (size_t)n, b->stream);
+    if (e == hipSuccess) {
+        const dim3 grid((unsigned)((ctx->geo.h + kDigestRows - 1) / kDigestRows), 3, (unsigned)b->n_pics);
+        digest_kernel<<<grid, 256, 0, b->stream>>>(b->d_pics, ctx->geo, which == 0 ? 1 : 0, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, b->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "p265r_batch_digest");
+    return p265r_batch_status(ctx, b);
 }
 
 int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {

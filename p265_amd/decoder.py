@@ -152,6 +152,7 @@ class _Lane:
 
     def __init__(self, key, ctx):
         self.key, self.ctx, self.lock = key, ctx, threading.Lock()
+        self.failed = False             # a batch of it failed: the context is closed, not cached
 
 
 # end-to-end defaults (tools/e2e_profile.py sweep on the GPU box, 128 x 1080p, 16 host threads; round 4,
@@ -179,10 +180,10 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT
     parser = bitstream.StreamParser(threads=threads, asynchronous=True)
     q = queue.Queue(maxsize=max(1, prefetch))
     done_q = queue.Queue()
-    slots = threading.Semaphore(max(1, depth))
+    depth = max(1, min(16, depth))     # (clamped first: the semaphore and the cleanup use the same value)
+    slots = threading.Semaphore(depth)
     stop = threading.Event()
     st = stats if stats is not None else StageTimes()
-    depth = max(1, min(4, depth))
 
     def produce():
         # asynchronous parsing: feed() submits the complete access units to the parser's workers
@@ -275,12 +276,19 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT
     rank = 0
 
     def retire(lane, b, group):
-        with lane.lock:
-            t0 = clock()
-            outs = lane.ctx.download(b)                         # waits for the batch, planes -> host
-            st.add("download_wait", clock() - t0)
-            b.free()
-        slots.release()
+        try:
+            with lane.lock:
+                t0 = clock()
+                try:
+                    outs = lane.ctx.download(b)                 # waits for the batch, planes -> host
+                except BaseException:
+                    lane.failed = True                          # closed at the end, never cached
+                    raise
+                finally:
+                    st.add("download_wait", clock() - t0)
+                    b.free()
+        finally:
+            slots.release()
         ready = []
         for d, planes in zip(group, outs):
             fr = DecodedFrame(poc=d.poc, output_rank=-1, decode_index=int(d.picture.meta["decode_index"]),
@@ -344,7 +352,7 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT
         t0 = clock()
         for ls in lanes.values():
             for lane in ls:
-                if cache_contexts:
+                if cache_contexts and not lane.failed:
                     _return_context(lane.key, lane.ctx)
                 else:
                     lane.ctx.close()

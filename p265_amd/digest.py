@@ -1,0 +1,34 @@
+"""Host restatement of the device picture digest (p265r_batch_digest, csrc/digest.h).
+
+digest(plane) = sum over the plane's 4-sample words (row y, word k, W/4 words per row) of
+mix64(word | (y * W/4 + k) << 32) mod 2^64, with mix64 the splitmix64 finalizer and word the
+little-endian 32-bit value of samples 4k..4k+3 of row y.  Position-keyed, so a changed, swapped
+or shifted sample changes it; a sum, so the device adds partial sums in any order.
+"""
+import numpy as np
+
+_M1 = np.uint64(0xbf58476d1ce4e5b9)
+_M2 = np.uint64(0x94d049bb133111eb)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * _M1
+    z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def plane_digest(plane):
+    """Digest of one uint8 plane [h][w] (w a multiple of 4) as a Python int."""
+    p = np.ascontiguousarray(plane, np.uint8)
+    h, w = p.shape
+    if w % 4:
+        raise ValueError("plane width %d is not a multiple of 4" % w)
+    words = p.view("<u4").astype(np.uint64).ravel()
+    pos = np.arange(words.size, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return int(_mix64(words | (pos << np.uint64(32))).sum(dtype=np.uint64))
+
+
+def picture_digest(planes):
+    """[Y, Cb, Cr] uint8 planes -> uint64 array of 3 digests (p265r_batch_digest's layout)."""
+    return np.array([plane_digest(pl) for pl in planes], np.uint64)

@@ -179,6 +179,18 @@ class ReconContext:
         (p265r_batch_status: the row kernel's sticky error word)."""
         _lib.check(self.lib.p265r_batch_status(self.handle, batch.handle), "p265r_batch_status")
 
+    def digest(self, batch, recon=False):
+        """Per-picture digests of the batch's planes after its last run, computed on the device
+        (p265r_batch_digest; no plane download): uint64 array [n_pictures, 3] (Y, Cb, Cr), equal to
+        digest.picture_digest() of the planes download() would return (recon: the reconstruction
+        before the in-loop filters).  Raises P265RError like status()."""
+        n = len(batch.pics)
+        out = np.zeros(3 * n, np.uint64)
+        _lib.check(self.lib.p265r_batch_digest(self.handle, batch.handle, 1 if recon else 0,
+                                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 3 * n),
+                   "p265r_batch_digest")
+        return out.reshape(n, 3)
+
     def sync(self):
         _lib.check(self.lib.p265r_sync(self.handle), "p265r_sync")
 

@@ -1,12 +1,13 @@
-"""bench.py's post-run output check (CPU): the verify path compares downloaded planes with the
-C oracle, and a mismatch turns into a non-zero exit code (the line's value is then no result)."""
+"""bench.py's post-run output check (CPU): every timed picture's device digest is compared with the
+digest of the C oracle's decode, a mismatch turns into a non-zero exit code (the line's value is then
+no result), and the host digest (p265_amd/digest.py) is the function csrc/digest.h computes."""
 import importlib.util
 import os
 
 import numpy as np
 
 from oracle import c_oracle
-from p265_amd import synth
+from p265_amd import digest, synth
 from p265_amd import records as R
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -19,6 +20,36 @@ def _bench():
     return mod
 
 
+def _mix64_py(z):
+    m = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & m
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & m
+    return z ^ (z >> 31)
+
+
+def test_plane_digest_is_the_documented_sum():
+    rng = np.random.default_rng(5)
+    plane = rng.integers(0, 256, (6, 12), dtype=np.uint8)
+    want = 0
+    for y in range(6):
+        for k in range(3):
+            word = int.from_bytes(bytes(plane[y, 4 * k:4 * k + 4]), "little")
+            want = (want + _mix64_py(word | (y * 3 + k) << 32)) & ((1 << 64) - 1)
+    assert digest.plane_digest(plane) == want
+
+
+def test_plane_digest_sees_position():
+    rng = np.random.default_rng(6)
+    plane = rng.integers(0, 256, (8, 16), dtype=np.uint8)
+    d0 = digest.plane_digest(plane)
+    swapped = plane.copy()
+    swapped[[2, 5]] = swapped[[5, 2]]                 # two rows swapped: same multiset of words
+    assert digest.plane_digest(swapped) != d0
+    flip = plane.copy()
+    flip[7, 15] ^= 1
+    assert digest.plane_digest(flip) != d0
+
+
 def test_pictures_to_check_covers_both_ends():
     b = _bench()
     assert b.pictures_to_check(512, 4) == [0, 1, 2, 3, 508, 509, 510, 511]
@@ -26,19 +57,18 @@ def test_pictures_to_check_covers_both_ends():
     assert b.pictures_to_check(8, 8) == list(range(8))
 
 
-def test_verify_accepts_the_oracle_output_and_flags_a_corrupted_download():
+def test_verify_accepts_the_oracle_digests_and_flags_a_corrupted_picture():
     b = _bench()
     params = R.make_params(pic_width=128, pic_height=64)
     uniq = [synth.make_picture(params, 31 + i) for i in range(2)]
     pics = [uniq[i % 2] for i in range(5)]
-    idx = b.pictures_to_check(len(pics), 2)
-    ref = {id(p): out for p, (_, out) in zip(uniq, c_oracle.decode(params, uniq, with_recon=False))}
-    got = {i: [np.array(pl) for pl in ref[id(pics[i])]] for i in idx}
-    n, bad = b.verify_planes(params, pics, got, threads=2)
-    assert (n, bad) == (4, [])
-    got[3][1][5, 7] ^= 1                              # one Cb sample of picture 3 off by one bit
-    n, bad = b.verify_planes(params, pics, got, threads=2)
-    assert (n, bad) == (4, [3])
+    want = {id(p): digest.picture_digest(out) for p, (_, out) in zip(uniq, c_oracle.decode(params, uniq, with_recon=False))}
+    got = np.stack([want[id(p)] for p in pics])       # what a correct device run returns
+    assert b.digest_mismatches(pics, want, got) == []
+    planes = [np.array(pl) for pl in c_oracle.decode(params, [pics[3]], with_recon=False)[0][1]]
+    planes[1][5, 7] ^= 1                              # one Cb sample of picture 3 off by one bit
+    got[3] = digest.picture_digest(planes)
+    assert b.digest_mismatches(pics, want, got) == [3]
     # the exit path: a failed check makes bench.py exit non-zero
     assert b.exit_code({"verified": {"ok": False, "mismatches": ["batch 0 picture 3"]}}) == 3
     assert b.exit_code({"verified": {"ok": True}}) == 0

@@ -171,3 +171,11 @@ def test_async_feed_reports_a_broken_picture_in_order():
     assert len(got) <= 2 and len(ref) >= 3
     for a, b in zip(got, ref):
         _same(a, b)
+    # the error comes once the pictures before it are taken; the broken picture is then dropped: the
+    # rest of the stream follows (a caller resyncs at the next IRAP) and the pending count drains
+    assert len(got) == 2
+    while p.pending:
+        got += p.wait()
+    assert [g.picture.meta["decode_index"] for g in got] == [0, 1] + list(range(3, len(ref)))
+    for a, b in zip(got[2:], ref[3:]):
+        _same(a, b)

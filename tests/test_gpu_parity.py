@@ -268,6 +268,60 @@ def test_pipelined_chip_filling_batches_phase_order(recon_mod):
             b.free()
 
 
+def test_pipelined_chip_filling_and_small_batches_mixed(recon_mod):
+    """One pipelined context runs a chip-filling batch (phase-ordered: residual + prep wait for the
+    last intra launch of any lane) interleaved with a small batch (all phases on its lane, not phase-
+    ordered): the chip-filling batch's re-runs must still wait for its OWN previous intra phase before
+    overwriting its residual pool and job lists.  Every picture of both batches is checked through
+    the device digest (p265r_batch_digest)."""
+    from p265_amd import digest
+    params = R.make_params(pic_width=64, pic_height=64)
+    distinct = [synth.make_picture(params, 970 + s, perf=bool(s % 2)) for s in range(4)]
+    pd = R.params_dict(params)
+    want = [digest.picture_digest(O.decode_picture(pd, p.as_oracle_dict())[1]) for p in distinct]
+    with recon_mod.ReconContext(params) as ctx:
+        n = int(ctx.describe()["num_cus"])
+        big = [distinct[i % 4] for i in range(n)]
+        small = [distinct[(i + 1) % 4] for i in range(4)]
+        ctx.set_pipeline(3)
+        bb, bs = ctx.upload(big), ctx.upload(small)
+        for _ in range(4):
+            ctx.run(bb)
+            ctx.run(bs)
+            ctx.run(bs)
+        ctx.sync()
+        for pics, b in ((big, bb), (small, bs)):
+            got = ctx.digest(b)
+            for i in range(len(pics)):
+                assert np.array_equal(got[i], want[distinct.index(pics[i])]), "picture %d of a %d-picture batch" % (i, len(pics))
+            b.free()
+
+
+def test_batch_digest_equals_host_digest(recon_mod):
+    """p265r_batch_digest (device) equals p265_amd/digest.py (host) on the oracle's planes, for the
+    output planes and the reconstruction, on a ragged batch with deblocking (so the two differ) and
+    odd picture sizes."""
+    from p265_amd import digest
+    big = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5)
+    sizes = [(264, 200), (128, 72), (40, 200), (264, 8)]
+    pics = []
+    for k, (w, h) in enumerate(sizes):
+        pp = R.pic_params(big, R.Picture(ctus=None, tbs=None, coef=None, size=(w, h)))
+        pic = synth.make_picture(pp, 990 + k, perf=bool(k % 2), deblocking=True)
+        pic.size = (w, h)
+        pics.append(pic)
+    with recon_mod.ReconContext(big) as ctx:
+        b = ctx.upload(pics)
+        ctx.run(b)
+        got, got_rec = ctx.digest(b), ctx.digest(b, recon=True)
+        b.free()
+    for i, pic in enumerate(pics):
+        rec_ref, out_ref = O.decode_picture(R.params_dict(R.pic_params(big, pic)), pic.as_oracle_dict())
+        assert np.array_equal(got[i], digest.picture_digest(out_ref)), "out %d" % i
+        assert np.array_equal(got_rec[i], digest.picture_digest(rec_ref)), "recon %d" % i
+        assert not np.array_equal(got[i], got_rec[i])
+
+
 @pytest.mark.parametrize("ctb_log2,deblocking", [(6, False), (5, False), (4, False), (6, "random"), (5, True)])
 def test_ragged_batch(recon_mod, schedule, ctb_log2, deblocking):
     """Pictures of different sizes in ONE batch (p265r_picture.pic_width / pic_height, up to the
