@@ -110,6 +110,14 @@ def parse():
     ap.add_argument("--frames", type=int, default=512, help="c3: 1080p pictures per GPU per step")
     ap.add_argument("--unique", type=int, default=4, help="c3: distinct synthetic pictures per rank (replicated)")
     ap.add_argument("--c5-frames", type=int, default=2, help="c5: 4K frames per step (x4 tile units, all ranks)")
+    ap.add_argument("--c5-batch-units", type=int, default=512,
+                    help="c5: tile units per resident batch of a rank -- a batch carries the rank's units of K = "
+                         "ceil(this / units per rank per step) consecutive steps (frames are independent), so one "
+                         "launch fills the GPU even at one unit per rank and step; 0 = one step per batch (the "
+                         "latency regime: 16 lanes side by side, one hardware queue each)")
+    ap.add_argument("--c5-world", type=int, default=0,
+                    help="c5: run rank 0's share of an N-rank job on this one GPU (dist.unit_shard(..., 0, N)); the "
+                         "line's value is then this GPU's rate (per_gpu_of_world = N), not a whole-job rate")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="resident batches run round-robin on this many HIP streams (p265r_set_pipeline; default "
                          "c3: 3 -- one batch's residual + prep phase beside another's loop filters; c5: 16 -- an "
@@ -244,7 +252,7 @@ def verify(ctxs, groups, a, threads, ran=None):
         want = {k: digest.picture_digest(r[1]) for k, r in zip(keys, ref)}
         want_sha = {k: sha_planes(r[1]) for k, r in zip(keys, ref)}
         distinct |= set(keys)
-        idx = pictures_to_check(len(gp), a.unique if a.workload == "c3" else len(gp))
+        idx = pictures_to_check(len(gp), a.unique if a.workload == "c3" else a.c5_units_per_step)
         for bi, b in enumerate(batches):
             if ran is not None and bi not in ran:
                 continue
@@ -341,46 +349,78 @@ def build_workload(a, rank, world):
     p4k = dist.broadcast_params(p4k)
     frames = [synth.make_picture(p4k, 4000 + f, perf=True, tiles=(2, 2), deblocking=a.deblocking)
               for f in range(a.c5_frames)]
-    mine = dist.unit_shard(a.c5_frames, 4, rank, world)
+    srank, sworld = (0, a.c5_world) if a.c5_world else (rank, world)
+    mine = dist.unit_shard(a.c5_frames, 4, srank, sworld)
     parts = {f: tiles.split(p4k, frames[f]) for f in sorted({f for f, _ in mine})}
     units = [parts[f][t] for f, t in mine]
     if not units:
-        raise RuntimeError("c5: rank %d has no tile unit (more ranks than units)" % rank)
+        raise RuntimeError("c5: rank %d of %d has no tile unit (more ranks than units)" % (srank, sworld))
     for tp, tpic, _ in units:
         tpic.meta["samples"] = int(tp["pic_width"]) * int(tp["pic_height"]) * 3 // 2
-    # the uneven tiles (1920 x 1088 top, 1920 x 1072 bottom) as ONE ragged batch: one context of the
-    # largest tile's size, every unit with its own size (p265r_picture.pic_width / pic_height)
-    groups = [(tiles.ragged_params(units), [tpic for _, tpic, _ in units])]
+    # K consecutive steps per batch: the same synthetic frames repeat every step (as C3 replicates its
+    # distinct pictures); the uneven tiles (1920 x 1088 top, 1920 x 1072 bottom) as ONE ragged batch:
+    # one context of the largest tile's size, every unit with its own size (p265r_picture.pic_width /
+    # pic_height)
+    k_steps = max(1, -(-a.c5_batch_units // len(units))) if a.c5_batch_units > 0 else 1
+    step_pics = [tpic for _, tpic, _ in units]
+    groups = [(tiles.ragged_params(units), step_pics * k_steps)]
     cols, rows = tiles.tile_grid(p4k, frames[0])
     ctus_all = a.c5_frames * sum((cols[i + 1] - cols[i]) * (rows[j + 1] - rows[j])
                                  for i in range(len(cols) - 1) for j in range(len(rows) - 1))
     pics = groups[0][1]
     params = groups[0][0]
     cfg = {"workload": "C5: 4K all-intra + %sSAO (CTU-row SAO kernel), 2x2 uniform tiles x %d frames = %d tile units "
-                       "per step over all ranks, %d on this rank" % ("deblocking + " if a.deblocking else "", a.c5_frames,
-                                                                     4 * a.c5_frames, len(pics)),
-           "pictures_per_gpu": len(pics), "units_per_step": 4 * a.c5_frames,
-           "ctus_per_picture": len(pics[0].ctus),
-           "tiles": sorted({"%dx%d" % tuple(p.size) for p in pics}),
-           "ctus_all_units": ctus_all,
+                       "per step over all ranks, %d on this rank; one batch = this rank's units of %d consecutive steps"
+                       % ("deblocking + " if a.deblocking else "", a.c5_frames, 4 * a.c5_frames, len(units), k_steps),
+           "pictures_per_gpu": len(pics), "units_per_step": 4 * a.c5_frames, "units_per_rank_step": len(units),
+           "steps_per_batch": k_steps, "ctus_per_picture": len(pics[0].ctus),
+           "tiles": sorted({"%dx%d" % tuple(p.size) for p in step_pics}),
+           "ctus_all_units": ctus_all, "ctus_rank_step": sum(len(p.ctus) for p in step_pics),
            "ctb": 64, "parallelism": "(frame, tile) units -> ranks x%d (dist.unit_shard); one ragged batch (one launch "
-                                     "per phase) for the uneven tile sizes" % world}
-    return groups, (params, pics, "tile units of 4K frames (%s)" % ", ".join(cfg["tiles"])), cfg
+                                     "per phase) for the uneven tile sizes" % sworld}
+    if a.c5_world:
+        cfg["simulated_world"] = {"world": a.c5_world, "rank": 0, "note": "rank 0's share of a %d-rank job on one GPU"
+                                  % a.c5_world}
+    return groups, (params, step_pics, "tile units of 4K frames (%s)" % ", ".join(cfg["tiles"])), cfg
+
+
+def c5_unit_latency(ctx, step_pics, runs):
+    """C5 unit latency: one step's tile units of this rank as ONE batch, run alone ``runs`` times
+    with per-phase HIP events; the units run concurrently (the row kernel gives every unit two
+    workgroups of its own, luma and chroma chains, on different CUs), so a run's time is one
+    unit's latency (the slowest unit's)."""
+    b = ctx.upload(step_pics)
+    try:
+        ctx.run(b)
+        ctx.sync()
+        ctx.set_timing(True)
+        for _ in range(runs):
+            ctx.run(b)
+        ctx.sync()
+        ctx.set_timing(False)
+        t = ctx.timings_total()
+    finally:
+        b.free()
+    n = max(1, t["runs"])
+    return {"one_batch_step": round(t["total_ms"] / n, 4), "intra": round(t["intra_ms"] / n, 4),
+            "residual": round(t["residual_ms"] / n, 4), "sao": round(t["sao_ms"] / n, 4), "units": len(step_pics),
+            "note": "one step's %d tile units of this rank as one batch, alone, %d runs" % (len(step_pics), n)}
 
 
 def main():
     a = parse()
+    c5_latency = a.workload == "c5" and a.c5_batch_units <= 0     # one step per batch, batches side by side
     if a.pipeline is None:
-        a.pipeline = 16 if a.workload == "c5" else 3
+        a.pipeline = 16 if c5_latency else 3
     if a.steps is None:
-        a.steps = 64 if a.workload == "c5" else 30
+        a.steps = 64 if c5_latency else (20 if a.workload == "c5" else 30)
     # one hardware queue per stream (the lanes + the upload stream): HIP's default 4 would put two C5
     # lanes behind each other (c5, 8 lanes: 3.0 M CTU/s at 4 queues, 8.4 M at 12; 16 lanes at 20 queues:
     # 16.4 M, every CU holding one unit's workgroup; c3 measured best
     # at the default: 43.4 vs 41.8 M at 8 queues -- its prep / residual streams then interleave).
     # Raised (never lowered) before this process first touches HIP (dist.init below); the GPU boxes
     # export the default 4 explicitly.
-    if a.workload == "c5":
+    if c5_latency:
         want = min(32, a.pipeline + 4)
         try:
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
@@ -407,6 +447,7 @@ def main():
     t0 = time.time()
     groups, (cpu_params, cpu_sample, cpu_what), cfg = build_workload(a, rank, world)
     gen_s = time.time() - t0
+    a.c5_units_per_step = cfg.get("units_per_rank_step", 0)
     pics = [p for _, g in groups for p in g]
 
     # one context per picture size (c3: one); each holds one resident batch per stream (same
@@ -458,8 +499,10 @@ def main():
 
     if a.workload == "c3":
         total_ctus = world * n_ctu * a.steps
-    else:                                  # every tile unit of the step, over all ranks
-        total_ctus = cfg["ctus_all_units"] * a.steps
+    elif a.c5_world:                       # this GPU's share of a simulated c5_world-rank job
+        total_ctus = n_ctu * a.steps
+    else:                                  # every tile unit of the batch's steps, over all ranks
+        total_ctus = cfg["ctus_all_units"] * cfg["steps_per_batch"] * a.steps
     value = total_ctus / elapsed
     tot_b, intra_b, res_b, sao_b = algorithmic_bytes(pics)
     launches_per_step = acc["intra_launches"] / a.steps
@@ -493,13 +536,12 @@ def main():
         "setup_s": round(gen_s, 1),
     }
     if a.workload == "c5":
-        out["unit_latency_ms"] = {
-            "one_batch_step": round(acc["total_ms"] / a.steps, 4),
-            "intra": round(acc["intra_ms"] / a.steps, 4),
-            "note": "the %d tile units of a rank's step are ONE batch (one launch per phase) and run concurrently "
-                    "(the row kernel gives every unit two workgroups of its own, luma and chroma chains, on "
-                    "different CUs), so the one-batch step time is one unit's latency (the slowest unit's); "
-                    "pipelined steps overlap" % len(pics)}
+        out["unit_latency_ms"] = c5_unit_latency(ctxs[0][0], cpu_sample, a.steps)
+        if a.c5_world:
+            out["per_gpu_of_world"] = a.c5_world
+            out["value_note"] = ("this GPU's rate for rank 0's share of a %d-rank job (%d of the %d tile units of every "
+                                 "step); the whole job's rate is %d x this when every rank holds as many units"
+                                 % (a.c5_world, cfg["units_per_rank_step"], cfg["units_per_step"], a.c5_world))
     if exp:
         out["experiment_env"] = exp
     if world > 1:

@@ -48,6 +48,10 @@ using namespace p265r;
 #ifndef P265R_PHASE_ORDER
 #define P265R_PHASE_ORDER 1        // pipelined contexts: one intra phase at a time; residual + prep overlap loop filters
 #endif
+#ifndef P265R_UP_STREAM
+#define P265R_UP_STREAM 1          // 1: upload stream created with the context; 2: created at the first upload
+                                   // (after the lanes of p265r_set_pipeline); 0: uploads on the context stream
+#endif
 #ifndef P265R_SPLIT_W16
 #define P265R_SPLIT_W16 1          // small split batches: W = 16 row kernel (0: the by-run W, A/B)
 #endif
@@ -520,7 +524,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = lane_stream_create(ctx, &ctx->stream);
     if (e == hipSuccess) ctx->lanes.push_back(ctx->stream);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
+    if (e == hipSuccess && P265R_UP_STREAM == 1) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
     if (e == hipSuccess) {
         int8_t ang[35];
         int16_t inv[35];
@@ -845,7 +849,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     // device image: host-filled ranges copied, everything else of [0, o_rec) zero, on the upload
     // stream (a reused allocation's previous batch completed before p265r_batch_free returned);
     // complete before returning (the staging buffer is refilled by the next upload)
-    hipStream_t st = ctx->up_stream;
+    if (P265R_UP_STREAM == 2 && !ctx->up_stream && e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
+    hipStream_t st = P265R_UP_STREAM ? ctx->up_stream : ctx->stream;
     e = hipMemcpyAsync(dbase, host, o_res, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(dbase + o_res, 0, o_jobs[0] - o_res, st);
     if (e == hipSuccess && jobs_bytes) e = hipMemcpyAsync(dbase + o_jobs[0], host + s_jobs, jobs_bytes, hipMemcpyHostToDevice, st);

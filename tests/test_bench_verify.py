@@ -73,3 +73,22 @@ def test_verify_accepts_the_oracle_digests_and_flags_a_corrupted_picture():
     assert b.exit_code({"verified": {"ok": False, "mismatches": ["batch 0 picture 3"]}}) == 3
     assert b.exit_code({"verified": {"ok": True}}) == 0
     assert b.exit_code({}) == 0                       # --no-verify: nothing claimed
+
+
+def test_c5_batches_carry_consecutive_steps():
+    """C5 workload: a rank's batch carries its units of K consecutive steps, so one launch fills the GPU
+    even at one unit per rank and step; --c5-world N reproduces rank 0's share of an N-rank job."""
+    import types
+    b = _bench()
+    a = types.SimpleNamespace(workload="c5", c5_frames=2, c5_batch_units=512, c5_world=8, deblocking=False)
+    groups, (_, step_pics, _), cfg = b.build_workload(a, 0, 1)
+    assert cfg["units_per_rank_step"] == 1 and cfg["steps_per_batch"] == 512
+    assert len(groups[0][1]) == 512 and len(step_pics) == 1
+    assert cfg["simulated_world"]["world"] == 8
+    a.c5_world, a.c5_batch_units = 0, 512
+    groups, (_, step_pics, _), cfg = b.build_workload(a, 0, 1)
+    assert cfg["units_per_rank_step"] == 8 and cfg["steps_per_batch"] == 64 and len(groups[0][1]) == 512
+    assert sorted(cfg["tiles"]) == ["1920x1072", "1920x1088"]
+    a.c5_batch_units = 0                              # latency regime: one step per batch
+    groups, _, cfg = b.build_workload(a, 0, 1)
+    assert cfg["steps_per_batch"] == 1 and len(groups[0][1]) == 8
