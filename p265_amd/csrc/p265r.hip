@@ -42,15 +42,19 @@ using namespace p265r;
 #ifndef P265R_EXPERIMENTS
 #define P265R_EXPERIMENTS 0
 #endif
+// Stream plan of pipelined contexts (round 5: one interleaved A/B of round 3's head against every round-4
+// step): the round-4 additions below each cost 5-8 % of the pipelined C3 step by adding
+// streams -- a process's streams map round-robin onto GPU_MAX_HW_QUEUES hardware queues (4), so every
+// extra stream changes which lanes' kernels queue behind which -- and are off (A/B macros only):
 #ifndef P265R_EARLY_RESIDUAL
-#define P265R_EARLY_RESIDUAL 1     // re-runs: residual + prep start when the batch's previous intra phase ends
+#define P265R_EARLY_RESIDUAL 0     // re-runs: residual + prep start when the batch's previous intra phase ends
 #endif
 #ifndef P265R_PHASE_ORDER
-#define P265R_PHASE_ORDER 1        // pipelined contexts: one intra phase at a time; residual + prep overlap loop filters
+#define P265R_PHASE_ORDER 0        // pipelined contexts: one intra phase at a time; residual + prep overlap loop filters
 #endif
 #ifndef P265R_UP_STREAM
-#define P265R_UP_STREAM 1          // 1: upload stream created with the context; 2: created at the first upload
-                                   // (after the lanes of p265r_set_pipeline); 0: uploads on the context stream
+#define P265R_UP_STREAM 0          // 0: a batch uploads on its own lane stream; 1: on an upload stream created with
+                                   // the context; 2: created at the first upload (after the lanes)
 #endif
 #ifndef P265R_SPLIT_W16
 #define P265R_SPLIT_W16 1          // small split batches: W = 16 row kernel (0: the by-run W, A/B)
@@ -850,7 +854,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     // stream (a reused allocation's previous batch completed before p265r_batch_free returned);
     // complete before returning (the staging buffer is refilled by the next upload)
     if (P265R_UP_STREAM == 2 && !ctx->up_stream && e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
-    hipStream_t st = P265R_UP_STREAM ? ctx->up_stream : ctx->stream;
+    hipStream_t st = P265R_UP_STREAM ? ctx->up_stream : b->stream;
     e = hipMemcpyAsync(dbase, host, o_res, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemsetAsync(dbase + o_res, 0, o_jobs[0] - o_res, st);
     if (e == hipSuccess && jobs_bytes) e = hipMemcpyAsync(dbase + o_jobs[0], host + s_jobs, jobs_bytes, hipMemcpyHostToDevice, st);
@@ -1295,10 +1299,14 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"phase_order\": %d, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
-        ctx->row_waves ? "fixed" : "batches of >= 1 picture per CU in a pipelined context: W=12, one intra launch at a time "
-                                   "(phase order); small batches (< 1 picture per CU: component split, W=16): side by side; "
-                                   "otherwise W=12 while no other lane has a run enqueued since the API synchronised it, "
-                                   "else pipe_waves",
+        ctx->row_waves ? "fixed" : (P265R_PHASE_ORDER
+                                   ? "batches of >= 1 picture per CU in a pipelined context: W=12, one intra launch at a time "
+                                     "(phase order); small batches (< 1 picture per CU: component split, W=16): side by side; "
+                                     "otherwise W=12 while no other lane has a run enqueued since the API synchronised it, "
+                                     "else pipe_waves"
+                                   : "small batches (< 1 picture per CU: component split, W=16); otherwise W=12 while no other "
+                                     "lane has a run enqueued since the API synchronised it, else pipe_waves (W=8, 80 VGPRs: "
+                                     "the other lanes' residual / prep / SAO waves fit beside it)"),
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
         ctx->pipeline, ctx->fork_prep, ctx->pipe_waves, hwq_env(), ctx->num_cus,
 #ifdef P265R_DEBUG_DIAG

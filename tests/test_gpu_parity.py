@@ -240,10 +240,10 @@ def test_pipelined_small_batches_eight_lanes(recon_mod):
                 np.testing.assert_array_equal(outs[k][i][c], ref[c], err_msg="set %d pic %d c%d" % (k, i, c))
 
 
-def test_pipelined_chip_filling_batches_phase_order(recon_mod):
-    """Batches of at least one picture per CU take the phase-ordered path (forked prep and
-    residual streams, one intra launch at a time, the next batch's residual phase beside the
-    previous one's loop filters): three such batches of 64x64 pictures, each run twice,
+def test_pipelined_chip_filling_batches(recon_mod):
+    """Batches of at least one picture per CU in a pipelined context (forked prep streams; after the
+    first run the W = 8 row kernel beside the other lanes' phases; the phase-ordered variant of round
+    4 is an A/B build, P265R_PHASE_ORDER): three such batches of 64x64 pictures, each run twice,
     interleaved; the first, a middle and the last picture of every batch equal the oracle."""
     params = R.make_params(pic_width=64, pic_height=64)
     distinct = [synth.make_picture(params, 950 + s, perf=bool(s % 2)) for s in range(4)]
@@ -269,10 +269,10 @@ def test_pipelined_chip_filling_batches_phase_order(recon_mod):
 
 
 def test_pipelined_chip_filling_and_small_batches_mixed(recon_mod):
-    """One pipelined context runs a chip-filling batch (phase-ordered: residual + prep wait for the
-    last intra launch of any lane) interleaved with a small batch (all phases on its lane, not phase-
-    ordered): the chip-filling batch's re-runs must still wait for its OWN previous intra phase before
-    overwriting its residual pool and job lists.  Every picture of both batches is checked through
+    """One pipelined context runs a chip-filling batch (forked prep stream) interleaved with a small
+    batch (all phases on its lane): every run of either must wait for its OWN previous intra phase
+    before overwriting its residual pool and job lists (with P265R_PHASE_ORDER builds the residual +
+    prep phase waits for the last intra launch of ANY lane, which a small batch's runs do not order).  Every picture of both batches is checked through
     the device digest (p265r_batch_digest)."""
     from p265_amd import digest
     params = R.make_params(pic_width=64, pic_height=64)
