@@ -11,7 +11,11 @@ CXX ?= g++
 FESRC := $(wildcard p265_amd/csrc/fe/*.cpp)
 FEHDR := $(wildcard p265_amd/csrc/fe/*.h) include/p265fe.h include/p265r.h
 
-all: p265_amd/libp265r.so p265_amd/libp265fe.so oracle
+all: p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so oracle
+
+# measurement helper (not the product path): the row kernel's job-loop issue ceiling (bench.py)
+p265_amd/libp265probe.so: p265_amd/csrc/issue_probe.hip
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -shared -Wall -o $@ $<
 
 # native syntax front-end (host C++, no GPU code)
 p265_amd/libp265fe.so: $(FESRC) $(FEHDR)
@@ -24,7 +28,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f p265_amd/libp265r.so p265_amd/libp265fe.so
+	rm -f p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -101,6 +101,47 @@ def issue_rates(workload, kernel_prefix, avg_ms):
             "peaks": "VALU 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 op; SALU 256 CUs x 2.4 GHz"}
 
 
+PROBE_MIX = {"valu": 131, "salu": 81, "lds": 15}     # p265_amd/csrc/issue_probe.hip, which = 0
+
+
+def issue_ceiling(device, avg_launch_ms, jobs_per_launch, num_cus, rates=None):
+    """Measured issue ceiling of the row kernel's job loop (p265_amd/libp265probe.so): the mix of
+    VALU / SALU / LDS instructions per job issued with no dependencies at the row kernel's occupancy
+    (24 waves per CU); -> CU-cycles per job at that ceiling, the row kernel's own CU-cycles per job
+    (launch time x the probe's measured clock x CUs / jobs), and their ratio."""
+    import ctypes
+    path = os.path.join(ROOT, "p265_amd", "libp265probe.so")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:
+        return {"error": "libp265probe.so: %s" % e}
+    fn = lib.p265probe_issue
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    jobs = 16384
+    res = {}
+    for which, name in enumerate(("mix", "valu_only", "salu_only", "lds_only")):
+        c, ms = ctypes.c_double(0), ctypes.c_double(0)
+        rc = fn(device, which, jobs, ctypes.byref(c), ctypes.byref(ms))
+        if rc:
+            return {"error": "p265probe_issue(%d) = %d" % (which, rc)}
+        res[name] = (c.value, ms.value)
+    c_mix, ms_mix = res["mix"]
+    clk = c_mix * jobs * 24 / (ms_mix * 1e-3)                      # the slowest wave spans the launch
+    row = avg_launch_ms * 1e-3 * clk * num_cus / max(1, jobs_per_launch)
+    out = {"probe_mix_per_job": PROBE_MIX, "ceiling_cu_cycles_per_job": round(c_mix, 1),
+           "valu_only": round(res["valu_only"][0], 1), "salu_only": round(res["salu_only"][0], 1),
+           "lds_only": round(res["lds_only"][0], 1), "clock_ghz": round(clk / 1e9, 3),
+           "jobs_per_launch": int(jobs_per_launch), "row_kernel_cu_cycles_per_job": round(row, 1),
+           "frac": round(c_mix / row, 3) if row else None,
+           "how": "p265_amd/csrc/issue_probe.hip: the job mix issued with no dependencies at 24 waves per CU, "
+                  "s_memtime cycles of the slowest wave; frac = that ceiling / the row kernel's CU-cycles per job"}
+    if rates:
+        out["profile_mix_per_job"] = {"valu": round(rates["valu_per_launch"] / jobs_per_launch, 1),
+                                      "salu": round(rates["salu_per_launch"] / jobs_per_launch, 1)}
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,8 +161,8 @@ def parse():
                          "line's value is then this GPU's rate (per_gpu_of_world = N), not a whole-job rate")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="resident batches run round-robin on this many HIP streams (p265r_set_pipeline; default "
-                         "c3: 3 -- one batch's residual + prep phase beside another's loop filters; c5: 16 -- an "
-                         "8-unit batch fills 16 CUs, so 16 whole batches run side by side)")
+                         "2 -- one batch's residual / prep / SAO phases beside the other's intra phase; c5 with "
+                         "--c5-batch-units 0: 16 -- an 8-unit batch fills 16 CUs, so 16 whole batches run side by side)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the bitstream -> planes end-to-end leg")
@@ -411,7 +452,9 @@ def main():
     a = parse()
     c5_latency = a.workload == "c5" and a.c5_batch_units <= 0     # one step per batch, batches side by side
     if a.pipeline is None:
-        a.pipeline = 16 if c5_latency else 3
+        # 2 lanes: with the prep stream of each lane, 4 streams on HIP's default 4 hardware queues, one
+        # queue each (round 5, same box: 2 lanes 5.30 ms per step, 3 lanes 5.77-5.80, 4 lanes 6.1-6.4)
+        a.pipeline = 16 if c5_latency else 2
     if a.steps is None:
         a.steps = 64 if c5_latency else (20 if a.workload == "c5" else 30)
     # one hardware queue per stream (the lanes + the upload stream): HIP's default 4 would put two C5
@@ -496,6 +539,7 @@ def main():
         assert t["runs"] == a.steps
         acc = t if acc is None else {k: acc[k] + t[k] for k in acc}
     knobs = ctxs[0][0].describe()
+    jl, jch = ctxs[0][0].job_count(ctxs[0][1][0])
 
     if a.workload == "c3":
         total_ctus = world * n_ctu * a.steps
@@ -529,6 +573,7 @@ def main():
                              "HBM: halving the quad jobs' LDS round trips at +10-15 % instructions was 18 % slower "
                              "(DESIGN.md §4, round 4); see issue_rates"},
         "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms),
+        "intra_jobs_per_launch": {"luma": jl, "chroma": jch},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
         "phase_gbs": {"residual": round(res_b / (acc["residual_ms"] / a.steps * 1e-3) / 1e9, 1),
                       "sao": round(sao_b / (acc["sao_ms"] / a.steps * 1e-3) / 1e9, 1) if acc["sao_ms"] else None,
@@ -555,6 +600,9 @@ def main():
         out["verified"] = v
     if rank == 0:
         out["roofline"]["achievable_copy_gbs"] = hip.copy_bandwidth_gbs(local)
+        if a.workload == "c3" and launches_per_step == 1:
+            out["roofline"]["issue"] = issue_ceiling(local, avg_launch_ms, jl + jch,
+                                                     int(knobs.get("num_cus", 256)), out["issue_rates"])
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         if py_base is not None:
             py_base.update(host_cores_total=host["host_cores_total"], cpu_model=host["cpu_model"])

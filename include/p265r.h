@@ -182,6 +182,10 @@ int  p265r_batch_status(p265r_ctx* ctx, p265r_batch* batch);
  * n = 3 * the batch's pictures.  Returns what p265r_batch_status returns afterwards.  Lets a
  * benchmark check every picture it timed.  No counterpart in the reference. */
 int  p265r_batch_digest(p265r_ctx* ctx, p265r_batch* batch, int which, uint64_t* out, int n);
+/* Intra jobs of the batch's last run (after job preparation: a 4x4 quad counts once, a Cb+Cr pair
+ * once), luma and chroma, summed over its pictures; waits for the batch's lane.  For measurement
+ * (bench.py: the row kernel's cycles per job).  No counterpart in the reference. */
+int  p265r_batch_job_count(p265r_ctx* ctx, p265r_batch* batch, uint64_t* luma, uint64_t* chroma);
 int  p265r_batch_free(p265r_ctx* ctx, p265r_batch* batch);
 
 /* Convenience: upload + run (asynchronous) ... */

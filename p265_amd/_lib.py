@@ -73,6 +73,7 @@ SIGNATURES = {
     "p265r_batch_download": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(PictureC), ctypes.c_int]),
     "p265r_batch_status": (ctypes.c_int, [_vp, _vp]),
     "p265r_batch_digest": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "p265r_batch_job_count": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "p265r_batch_free": (ctypes.c_int, [_vp, _vp]),
     "p265r_submit": (ctypes.c_int, [_vp, ctypes.POINTER(PictureC), ctypes.c_int]),
     "p265r_wait": (ctypes.c_int, [_vp]),

@@ -26,8 +26,8 @@
 namespace p265r {
 
 // Intra job record written by intra_prep_kernel (layout: intra_prep.h).
-struct IntraJob {
-    uint32_t w[8];
+struct IntraJob {                // 24 bytes (intra_prep.h documents the words)
+    uint32_t w[6];
 };
 
 struct DevPic {                 // per picture, device-resident table

@@ -22,7 +22,7 @@
 
 namespace p265r {
 
-// 32-byte job record (w6, w7 reserved, 0).
+// 24-byte job record (words w0..w5; round 5: 32 -> 24 B, the quads' residuals as base + codes).
 //  w0: [0,13) LDS offset of the TB origin in WaveLds (luma yr*64+xr, chroma 4096+yr*32+xr)
 //      [13,15) log2-2  [15,17) component mask (0 luma, 1 Cb, 2 Cr, 3 Cb+Cr)  [17,23) mode
 //      23 PCM  [24,26) filter (0 none, 1 [1 2 1], 2 strong candidate)
@@ -46,14 +46,16 @@ namespace p265r {
 //  w1: [0,6) mode q2  [6,12) mode q3  12 / 13: none for q2 / q3  [14,19) fa q0  [19,24) la q0
 //      [24,29) fa q1
 //  w2: [0,5) la q1  [5,10) fa q2  [10,15) la q2  [15,20) fa q3  [20,25) la q3
-//  w3, w4, w6, w7: residual offsets of q0, q1, q2, q3 (as w3 above)
+//  w3: residual base offset; w4: 4-bit code per sub-TB q at bit 4q, residual = w3 + 16 * code, code 15 =
+//      the zero block (DevPic::zero_off): coded 4x4 luma TBs of one class sit in decode order in
+//      16-sample slots, so the region's coded sub-TBs are consecutive (else no quad)
 // Chroma 4x4 QUAD job (w5 has J5_FAST | J5_QUAD, w0 component mask 3): the four fast Cb+Cr
 // 4x4 pairs of one 8x8 chroma region (four consecutive TUs in decode order), reconstructed
 // by intra_rows.h recon_quad<true> with Cb and Cr packed in the 16-bit halves of one lane.
 //  w0: as the luma quad, [15,17) = 3, [0,13) LDS offset of the Cb region origin
 //  w1, w2: as the luma quad (modes, none bits, fa / la per sub-TB)
 //  w3: residual base offset; w4: 4-bit code per (sub-TB q, component h) at bit 8q + 4h,
-//      residual = w3 + 16 * code, code 15 = the zero block (w6 = zero_off)
+//      residual = w3 + 16 * code, code 15 = the zero block (DevPic::zero_off)
 // (struct IntraJob: intra.h)
 
 enum : uint32_t {
@@ -69,21 +71,44 @@ enum : uint32_t {
 constexpr uint32_t kJ5Bit32 = 1u << 16;
 struct LumaJobLds { uint32_t w0, w2, w3, w5; };
 
-// the four jobs at slots s..s+3 are the fast 4x4 luma TBs of one 8x8 region, in z-order
-// (straight-line: every lane of the prep wave evaluates it; bitwise & instead of early returns)
-__device__ __forceinline__ bool quad_jobs(const LumaJobLds* j) {
+// residual base + 4-bit codes of n offsets (code 15 = the zero block): the coded ones must sit in
+// 16-sample slots within 14 slots of their minimum (straight-line, bitwise &)
+template <int N>
+__device__ __forceinline__ bool quad_codes(const uint32_t* off, uint32_t zero_off, uint32_t& base, uint32_t& codes) {
+    int32_t mn = INT32_MAX;
+#pragma unroll
+    for (int i = 0; i < N; ++i) mn = off[i] != zero_off ? min(mn, (int32_t)off[i]) : mn;
+    base = mn == INT32_MAX ? zero_off : (uint32_t)mn;
+    codes = 0;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const uint32_t d = off[i] - (uint32_t)mn;                 // >= 0 for the coded ones: mn is their minimum
+        const bool z = off[i] == zero_off;
+        ok &= z | (((d & 15u) == 0u) & (d <= 14u * 16u));
+        codes |= (z ? 15u : (d >> 4) & 15u) << (4 * i);
+    }
+    return ok;
+}
+
+// the four jobs at slots s..s+3 are the fast 4x4 luma TBs of one 8x8 region, in z-order, and their
+// residuals are addressable as base + 16 * code (straight-line: every lane of the prep wave
+// evaluates it; bitwise & instead of early returns)
+__device__ __forceinline__ bool quad_jobs(const LumaJobLds* j, uint32_t zero_off, uint32_t& base, uint32_t& codes) {
     const uint32_t o = j[0].w0 & 0x1fffu;
     bool ok = ((o & 7u) | ((o >> 6) & 7u)) == 0u;                  // region origin on the 8x8 grid
+    uint32_t off[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t w0 = j[i].w0;
         ok &= ((j[i].w5 & J5_FAST) != 0u) & (((w0 >> 13) & 15u) == 0u) &    // fast, 4x4, luma
               ((w0 & 0x1fffu) == o + (uint32_t)((i & 1) * 4 + (i >> 1) * 256));
+        off[i] = j[i].w3;
     }
-    return ok;
+    return ok & quad_codes<4>(off, zero_off, base, codes);
 }
 
-__device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j) {
+__device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j, uint32_t base, uint32_t codes) {
     uint32_t mode[4], none[4], fa[4], la[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -96,11 +121,9 @@ __device__ __forceinline__ IntraJob make_quad(const LumaJobLds* j) {
     q.w[0] = (j[0].w0 & 0x1fffu) | mode[0] << 17 | mode[1] << 23 | none[0] << 29 | none[1] << 30;
     q.w[1] = mode[2] | mode[3] << 6 | none[2] << 12 | none[3] << 13 | fa[0] << 14 | la[0] << 19 | fa[1] << 24;
     q.w[2] = la[1] | fa[2] << 5 | la[2] << 10 | fa[3] << 15 | la[3] << 20;
-    q.w[3] = j[0].w3;
-    q.w[4] = j[1].w3;
+    q.w[3] = base;
+    q.w[4] = codes;
     q.w[5] = J5_FAST | J5_QUAD;
-    q.w[6] = j[2].w3;
-    q.w[7] = j[3].w3;
     return q;
 }
 
@@ -122,22 +145,10 @@ __device__ __forceinline__ bool cquad_jobs(const ChromaJobLds* j, uint32_t zero_
         off[2 * i] = j[i].w3;
         off[2 * i + 1] = j[i].w4;
     }
-    int32_t mn = INT32_MAX;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) mn = off[i] != zero_off ? min(mn, (int32_t)off[i]) : mn;
-    base = mn == INT32_MAX ? zero_off : (uint32_t)mn;
-    codes = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t d = off[i] - (uint32_t)mn;                 // >= 0 for the coded ones: mn is their minimum
-        const bool z = off[i] == zero_off;
-        ok &= z | (((d & 15u) == 0u) & (d <= 14u * 16u));
-        codes |= (z ? 15u : (d >> 4) & 15u) << (4 * i);            // i = 2q + h -> bit 8q + 4h
-    }
-    return ok;
+    return ok & quad_codes<8>(off, zero_off, base, codes);        // i = 2q + h -> bit 8q + 4h
 }
 
-__device__ __forceinline__ IntraJob make_cquad(const ChromaJobLds* j, uint32_t base, uint32_t codes, uint32_t zero_off) {
+__device__ __forceinline__ IntraJob make_cquad(const ChromaJobLds* j, uint32_t base, uint32_t codes) {
     uint32_t mode[4], none[4], fa[4], la[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -153,8 +164,6 @@ __device__ __forceinline__ IntraJob make_cquad(const ChromaJobLds* j, uint32_t b
     q.w[3] = base;
     q.w[4] = codes;
     q.w[5] = J5_FAST | J5_QUAD;
-    q.w[6] = zero_off;
-    q.w[7] = 0;
     return q;
 }
 
@@ -173,6 +182,15 @@ __device__ __forceinline__ uint4 prep_ld16(const void* p) {
 __device__ __forceinline__ void prep_st16(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     *(__attribute__((address_space(1))) prep_u4*)p = prep_u4{a, b, c, d};
 }
+typedef unsigned int prep_u2 __attribute__((ext_vector_type(2)));
+// one 24-B job record: three 8-B global stores (records are 8-B aligned: a 16-B store would straddle
+// a 16-B boundary on every other record)
+__device__ __forceinline__ void prep_job_store(IntraJob* dst, const IntraJob& J) {
+    typedef __attribute__((address_space(1))) prep_u2 gu2;
+    *(gu2*)(&dst->w[0]) = prep_u2{J.w[0], J.w[1]};
+    *(gu2*)(&dst->w[2]) = prep_u2{J.w[2], J.w[3]};
+    *(gu2*)(&dst->w[4]) = prep_u2{J.w[4], J.w[5]};
+}
 
 // grid (CTUs, pictures), 64 threads: one wave per CTU walks its TBs 64 at a time.  A CTU's
 // job list is [chroma jobs][luma jobs]; both are staged in LDS (luma words 0, 1, 2, 3, 5, at
@@ -184,7 +202,7 @@ constexpr int kPrepChunks = (kMaxCtuLuma + kMaxCtuChroma + 63) / 64;   // TB rec
 __device__ __forceinline__ IntraJob luma_job(const LumaJobLds& l, uint32_t zero_off, uint32_t w1) {
     IntraJob J;
     J.w[0] = l.w0; J.w[1] = w1; J.w[2] = l.w2; J.w[3] = l.w3;
-    J.w[4] = zero_off; J.w[5] = l.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
+    J.w[4] = zero_off; J.w[5] = l.w5 & ~kJ5Bit32;
     return J;
 }
 // job word w1 of a staged job: intraPredAngle | |invAngle| << 8 (c_angw), availability bit 32 << 21;
@@ -377,16 +395,12 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const uint32_t w1 = job_w1(c.w0, c.w5, angv);
         IntraJob J;
         if (hd) {
-            J = make_cquad(sc + sq, qb, qc, P.zero_off);
+            J = make_cquad(sc + sq, qb, qc);
         } else {
             J.w[0] = c.w0; J.w[1] = w1; J.w[2] = c.w2; J.w[3] = c.w3;
-            J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32; J.w[6] = J.w[7] = 0;
+            J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32;
         }
-        if (emit) {
-            uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + rank(me_));
-            prep_st16(dst, J.w[0], J.w[1], J.w[2], J.w[3]);
-            prep_st16(dst + 1, J.w[4], J.w[5], J.w[6], J.w[7]);
-        }
+        if (emit) prep_job_store(jobs + c_out + rank(me_), J);
         c_out += __popcll(me_);
     }
     int n_out = 0;
@@ -395,19 +409,16 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const int s = base + lane;
         const bool valid = s < n_luma;
         const int s1 = min(s, n_luma - 1), sq = min(s, kMaxCtuLuma - 4);
-        const bool hd = ((g.quad & 1) != 0) & (s + 3 < n_luma) & quad_jobs(sj + sq);
+        uint32_t qb = 0, qc = 0;
+        const bool hd = ((g.quad & 1) != 0) & (s + 3 < n_luma) & quad_jobs(sj + sq, P.zero_off, qb, qc);
         const unsigned long long H = __ballot(hd);
         const bool emit = valid & !((absorbed_mask(H, hp) >> lane) & 1ull);
         hp = H;
         const unsigned long long me_ = __ballot(emit);
         const LumaJobLds l = sj[s1];
         const uint32_t w1 = job_w1(l.w0, l.w5, angv);
-        const IntraJob J = hd ? make_quad(sj + sq) : luma_job(l, P.zero_off, w1);
-        if (emit) {
-            uint4* dst = reinterpret_cast<uint4*>(jobs + c_out + n_out + rank(me_));
-            prep_st16(dst, J.w[0], J.w[1], J.w[2], J.w[3]);
-            prep_st16(dst + 1, J.w[4], J.w[5], J.w[6], J.w[7]);
-        }
+        const IntraJob J = hd ? make_quad(sj + sq, qb, qc) : luma_job(l, P.zero_off, w1);
+        if (emit) prep_job_store(jobs + c_out + n_out + rank(me_), J);
         n_out += __popcll(me_);
     }
     if (lane == 0) *(__attribute__((address_space(1))) uint32_t*)(P.jcount + addr) = (uint32_t)n_out | (uint32_t)c_out << 16;

@@ -34,10 +34,10 @@ namespace p265r {
 #define P265R_SPIN_SLEEP 8
 #endif
 
-// SGPR bases of the job loop (LDS base, angle tables, Cb line) behind opaque s_mov copies per job (1), or
-// left to the compiler (0, A/B)
+// SGPR bases of the job loop (LDS base, angle tables, Cb line) behind opaque s_mov copies per job (1, A/B),
+// or left to the compiler (0: round 5, with 24-B job records, 5.26-5.27 vs 5.30 ms per pipelined step)
 #ifndef P265R_OPAQUE_S
-#define P265R_OPAQUE_S 1
+#define P265R_OPAQUE_S 0
 #endif
 
 // intraPredAngle 0 (modes 10 / 26) as plain copies in the fast paths (0 = the generic angular code)
@@ -55,6 +55,10 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint4 ld16(const void* p) {
     const u32x4_t v = *reinterpret_cast<const P265R_GLOBAL u32x4_t*>(gptr(p));
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld8(const void* p) {
+    const u32x2_t v = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(p));
+    return make_uint2(v.x, v.y);
 }
 // make every 32-bit word of a (wave-uniform) struct provably uniform: SGPRs, scalar branches
 template <typename T>
@@ -977,6 +981,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         const p265r_ctu* ctus = uniform(gload(&Pp->ctus));
         const IntraJob* jobs = uniform(gload(&Pp->jobs));
         const uint32_t* jcount = uniform(gload(&Pp->jcount));
+        const int zero_res = __builtin_amdgcn_readfirstlane((int)*gptr(&Pp->zero_off));   // the zero block
         // this picture's CTU grid and plane size (a ragged batch: DevPic::wh); the row queue, progress
         // words and line buffers keep the context's layout
         int pwc = g.wc, phc = g.hc, pw = g.w, ph = g.h;
@@ -1024,7 +1029,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             else __builtin_amdgcn_s_setprio(0);
         }
 #endif
-        uint4 rec0 = make_uint4(0, 0, 0, 0), rec1 = rec0;
+        uint4 rec0 = make_uint4(0, 0, 0, 0);
+        uint2 rec1 = make_uint2(0, 0);
         bool pre = false;                                  // rec0 / rec1 hold this CTU's first records
         for (int cx = 0; cx < pwc; ++cx) {
             // ---- wait for the row above (2-CTU lag) -------------------------------------
@@ -1069,13 +1075,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const bool pr = (w0 >> 15) & 3u;
                 return resid + (int)(pr && lane >= 32 ? w4 : w3) + (pr ? (lane & 31) : lane);
             };
-            // job records: 64 at a time into two VGPRs per lane, read per job with v_readlane
+            // job records (24 B): 64 at a time into six VGPRs per lane, read per job with v_readlane
             // (scalar loads were measured slower: their lgkmcnt waits serialise with the LDS
             // traffic of the job)
             struct JobS { uint32_t w0, w1, w2, w3, w4, w5; };
             auto refill = [&](int base) {
-                if (base + lane < nt) { rec0 = ld16(&jl[base + lane].w[0]); rec1 = ld16(&jl[base + lane].w[4]); }
-                else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
+                if (base + lane < nt) { rec0 = ld16(&jl[base + lane].w[0]); rec1 = ld8(&jl[base + lane].w[4]); }
+                else { rec0 = make_uint4(0, 0, 0, 0); rec1 = make_uint2(0, 0); }
             };
             auto sjob = [&](int i) {
                 const int l = i & 63;
@@ -1089,22 +1095,17 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             // across the loop and cost ~10 register copies per job
             u32x2_t rn = {0u, 0u};
             auto issue = [&](const JobS& j, int ji) -> u32x2_t {   // residual loads of job j (index ji)
-                if ((j.w5 & J5_QUAD) && ((j.w0 >> 15) & 3u)) {              // chroma quad: Cb | Cr << 16 of (x, y)
-                    const int l = ji & 63;
-                    const int zero = __builtin_amdgcn_readlane(rec1.z, l);      // w6 = zero_off
-                    const int q = ((lane >> 4) & 2) | ((lane >> 2) & 1);
-                    const uint32_t codes = j.w4 >> (8 * q);
+                if (j.w5 & J5_QUAD) {                       // quads: residual = w3 + 16 * code (15: the zero block)
+                    const int q = ((lane >> 4) & 2) | ((lane >> 2) & 1);    // sub-TB of sample (x, y) of the 8x8 region
                     const int i = ((lane >> 1) & 12) + (lane & 3);          // sample index in the 4x4 sub-TB
-                    auto at = [&](uint32_t code) { return (code == 15u ? zero : (int)j.w3 + (int)(code << 4)) + i; };
-                    const uint32_t cb = (uint16_t)*gptr(resid + at(codes & 15u));
-                    const uint32_t cr = (uint16_t)*gptr(resid + at((codes >> 4) & 15u));
-                    return u32x2_t{cb, cr};     // packed at use: no wait here
-                } else if (j.w5 & J5_QUAD) {                                // 4x4 quad: sample (x, y) of the 8x8 region
-                    const int l = ji & 63;
-                    const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane(rec1.z, l);
-                    const uint32_t w7 = (uint32_t)__builtin_amdgcn_readlane(rec1.w, l);
-                    const uint32_t o = (lane & 32) ? ((lane & 4) ? w7 : w6) : ((lane & 4) ? j.w4 : j.w3);
-                    return u32x2_t{(uint32_t)(int)*gptr(resid + (int)o + ((lane >> 1) & 12) + (lane & 3)), 0u};
+                    auto at = [&](uint32_t code) { return (code == 15u ? zero_res : (int)j.w3 + (int)(code << 4)) + i; };
+                    if ((j.w0 >> 15) & 3u) {                                // chroma: Cb | Cr << 16, codes at 8q + 4h
+                        const uint32_t codes = j.w4 >> (8 * q);
+                        const uint32_t cb = (uint16_t)*gptr(resid + at(codes & 15u));
+                        const uint32_t cr = (uint16_t)*gptr(resid + at((codes >> 4) & 15u));
+                        return u32x2_t{cb, cr};     // packed at use: no wait here
+                    }
+                    return u32x2_t{(uint32_t)(int)*gptr(resid + at((j.w4 >> (4 * q)) & 15u)), 0u};
                 } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 15u) == 13u) { // Cb+Cr 8x8: Cb | Cr << 16 of sample lane
                     const uint32_t cb = (uint16_t)*gptr(resid + (int)j.w3 + lane);
                     const uint32_t cr = (uint16_t)*gptr(resid + (int)j.w4 + lane);
@@ -1220,8 +1221,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int nc2 = (int)(jc2 >> 16);
                 const int nt2 = comp ? nc2 : (int)(jc2 & 0xffffu);
                 const IntraJob* jl2 = jobs + tb2 + (comp ? 0 : nc2);
-                if (lane < nt2) { rec0 = ld16(&jl2[lane].w[0]); rec1 = ld16(&jl2[lane].w[4]); }
-                else { rec0 = make_uint4(0, 0, 0, 0); rec1 = rec0; }
+                if (lane < nt2) { rec0 = ld16(&jl2[lane].w[0]); rec1 = ld8(&jl2[lane].w[4]); }
+                else { rec0 = make_uint4(0, 0, 0, 0); rec1 = make_uint2(0, 0); }
                 pre = true;
             }
             P265R_TRACE(5 | (cx << 8) | (r << 16));

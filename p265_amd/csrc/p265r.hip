@@ -1213,6 +1213,21 @@ int p265r_batch_digest(p265r_ctx* ctx, p265r_batch* b, int which, uint64_t* out,
     return p265r_batch_status(ctx, b);
 }
 
+int p265r_batch_job_count(p265r_ctx* ctx, p265r_batch* b, uint64_t* luma, uint64_t* chroma) {
+    if (!ctx || !b || !luma || !chroma) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    // per CTU slot: luma jobs | chroma jobs << 16 (intra_prep.h), context-size slots per picture
+    const size_t n = (size_t)ctx->n_ctus * b->n_pics;
+    std::vector<uint32_t> jc(n);
+    HIP_TRY(hipMemcpy(jc.data(), b->h_pics[0].jcount, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    uint64_t l = 0, c = 0;
+    for (uint32_t w : jc) { l += w & 0xffffu; c += w >> 16; }
+    *luma = l;
+    *chroma = c;
+    return P265R_OK;
+}
+
 int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     (void)hipSetDevice(ctx->device);

@@ -191,6 +191,13 @@ class ReconContext:
                    "p265r_batch_digest")
         return out.reshape(n, 3)
 
+    def job_count(self, batch):
+        """(luma, chroma) intra jobs of the batch's last run (p265r_batch_job_count)."""
+        lu, ch = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _lib.check(self.lib.p265r_batch_job_count(self.handle, batch.handle, ctypes.byref(lu), ctypes.byref(ch)),
+                   "p265r_batch_job_count")
+        return int(lu.value), int(ch.value)
+
     def sync(self):
         _lib.check(self.lib.p265r_sync(self.handle), "p265r_sync")
 
