@@ -14,12 +14,25 @@ import shutil
 import sys
 
 
+def kname(full):
+    """Kernel name without its argument list ('(anonymous namespace)' prefixes kept)."""
+    full = full.strip()
+    if full.endswith(")"):
+        depth = 0
+        for i in range(len(full) - 1, -1, -1):
+            depth += full[i] == ")"
+            depth -= full[i] == "("
+            if depth == 0:
+                return full[:i]
+    return full
+
+
 def per_kernel(path):
     rows = list(csv.DictReader(open(path)))
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     n = collections.defaultdict(collections.Counter)
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0]
+        k = kname(r["Kernel_Name"])
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         n[k][r["Counter_Name"]] += 1
     return {k: {c: v / n[k][c] for c, v in d.items()} for k, d in agg.items()}
@@ -31,7 +44,7 @@ def isolated_avg(path):
     steps on one batch alone for the phase times; only the latter give a kernel's own
     duration (an overlapped dispatch's span includes waiting for CU slots)."""
     rows = [r for r in csv.DictReader(open(path)) if r["Kind"] == "KERNEL_DISPATCH"]
-    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]) for r in rows)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kname(r["Kernel_Name"])) for r in rows)
     out = collections.defaultdict(list)
     for i, (a, b, name) in enumerate(iv):
         prev_end = max((e for _, e, _ in iv[:i]), default=-1)
@@ -61,7 +74,7 @@ def main(src, tag):
              "| kernel | calls | avg ms (isolated, n) | avg all ms | FETCH KB | WRITE KB | corrected traffic GB (2F+W) | VALU/wave | SALU/wave | LDS/wave |",
              "|---|---|---|---|---|---|---|---|---|---|"]
     for s in stats:
-        name = s["Name"].split("(")[0]
+        name = kname(s["Name"])
         if name.startswith("__amd"):
             continue
         f, w = fe.get(name, {}).get("FETCH_SIZE", 0.0), wr.get(name, {}).get("WRITE_SIZE", 0.0)
