@@ -1,8 +1,8 @@
 #!/bin/bash
 # One GPU call: the whole -m gpu suite (verbose, per-test timeout), then optional bench lines
 # (BENCHES: ';'-separated bench.py argument lists) and an interleaved A/B of the bench over the
-# libraries named in LIBS (tools/ab_libs2.sh).
-#   BENCHES="--workload c5 --steps 10;--steps 20 --warmup 5" LIBS="base default" REPS=3 bash tools/gpu_round.sh
+# configurations in CFGS (tools/ab.sh).
+#   BENCHES="--workload c5 --steps 10;--steps 20 --warmup 5" CFGS="base|-||;v|variant||" REPS=3 bash tools/gpu_round.sh
 set -e
 mkdir -p gpurun_out
 if [ -z "$NO_TESTS" ]; then
@@ -19,5 +19,5 @@ import json
 d=json.loads([l for l in open('gpurun_out/bench_$i.log') if l.startswith('{')][-1])
 print('bench $i', '$args', '%.0f CTU/s %.3f ms/step' % (d['value'], d['ms_per_step']), d.get('phases_ms_per_step'), 'verified', d.get('verified', {}).get('ok'), d.get('unit_latency_ms', ''))"
 done
-[ -n "$LIBS" ] && bash tools/ab_libs2.sh
+[ -n "$CFGS" ] && bash tools/ab.sh
 exit 0
