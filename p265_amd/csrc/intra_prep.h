@@ -105,6 +105,9 @@ __device__ __forceinline__ bool quad_jobs(const LumaJobLds* j, uint32_t zero_off
               ((w0 & 0x1fffu) == o + (uint32_t)((i & 1) * 4 + (i >> 1) * 256));
         off[i] = j[i].w3;
     }
+    // (sub-TBs 1-3 always see the earlier sub-TBs of the region: intra_rows.h quad_stage handles "no
+    // reference available" for the first stage only)
+    ok &= ((j[1].w0 | j[2].w0 | j[3].w0) & J_NONE) == 0u;
     return ok & quad_codes<4>(off, zero_off, base, codes);
 }
 
@@ -145,6 +148,7 @@ __device__ __forceinline__ bool cquad_jobs(const ChromaJobLds* j, uint32_t zero_
         off[2 * i] = j[i].w3;
         off[2 * i + 1] = j[i].w4;
     }
+    ok &= ((j[1].w0 | j[2].w0 | j[3].w0) & J_NONE) == 0u;        // (as quad_jobs)
     return ok & quad_codes<8>(off, zero_off, base, codes);        // i = 2q + h -> bit 8q + 4h
 }
 

@@ -437,11 +437,46 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
         }
     };
     int pred;
-    if (mode == 0) {
+    // angular modes first (the most frequent path tests one condition: modes 2..34)
+    if (mode >= 2) {
+        if (P265R_HV_FAST && (TAB ? (mode & ~16) == 10 : (angw & 0xffu) == 0u)) {
+            // modes 10 / 26 (intraPredAngle 0): a copy of the column left / the row above, plus the
+            // luma boundary smoothing of 8.4.4.2.6 (fast jobs are n < 32) - no projection arithmetic
+            const bool vert = mode >= 18;
+            pred = ref(vert ? 2 * n + 1 + x : 2 * n - 1 - y);
+            if (!PAIR) {
+                const int b = ref(vert ? 2 * n - 1 - y : 2 * n + 1 + x);
+                const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
+                pred = (vert ? x : y) == 0 ? edge : pred;
+            }
+        } else if (TAB) {
+            const int a = __builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), v);
+            const int b = __builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), v);
+            pred = (__mul24((int)(angw >> 24), a) + __mul24((int)((angw >> 16) & 0xffu), b) + 16) >> 5;
+        } else {
+            const int ang = (int)(int8_t)(angw & 0xffu);
+            const int ia = ang_inv(angw);
+            const bool vert = mode >= 18;
+            const int ns = vert ? -1 : 1;
+            const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
+            const int pa = __mul24(along + 1, ang);
+            const int idx = pa >> 5, fact = pa & 31;
+            const int nr0 = -1 - across - idx;                       // -(iIdx + across + 1)
+            const bool bflt = !P265R_HV_FAST && !PAIR && (mode == 26 || mode == 10);   // HV_FAST: copies above
+            const int k1 = ang_ref<2 * n>(nr0 - 1, ia, ns);          // computed unconditionally: a select, no branch
+            const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : k1;
+            const int a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(i1);
+            pred = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;   // = a when iFact = 0 (b then unused)
+            if (bflt) {                                              // modes 26 / 10, luma: boundary smoothing
+                const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
+                pred = (vert ? x : y) == 0 ? edge : pred;
+            }
+        }
+    } else if (mode == 0) {
         const int lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
         pred = (__mul24(n - 1 - x, lft) + __mul24(x + 1, uref(3 * n + 1)) + __mul24(n - 1 - y, top) +
                 __mul24(y + 1, uref(n - 1)) + n) >> (LOG2 + 1);
-    } else if (mode == 1) {
+    } else {
         const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
         // luma: the edge samples' bpermutes go out first, their latency under the DPP reduction
         const int lft = PAIR ? 0 : ref(2 * n - 1 - y), top = PAIR ? 0 : ref(2 * n + 1 + x);
@@ -452,38 +487,6 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
             // (lft + 2dc + top + 2) >> 2 at (0,0); one-sided (3dc + side + 2) >> 2 on row 0 / column 0
             const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
             pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
-        }
-    } else if (P265R_HV_FAST && (TAB ? (mode & ~16) == 10 : (angw & 0xffu) == 0u)) {
-        // modes 10 / 26 (intraPredAngle 0): a copy of the column left / the row above, plus the
-        // luma boundary smoothing of 8.4.4.2.6 (fast jobs are n < 32) - no projection arithmetic
-        const bool vert = mode >= 18;
-        pred = ref(vert ? 2 * n + 1 + x : 2 * n - 1 - y);
-        if (!PAIR) {
-            const int b = ref(vert ? 2 * n - 1 - y : 2 * n + 1 + x);
-            const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
-            pred = (vert ? x : y) == 0 ? edge : pred;
-        }
-    } else if (TAB) {
-        const int a = __builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), v);
-        const int b = __builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), v);
-        pred = (__mul24((int)(angw >> 24), a) + __mul24((int)((angw >> 16) & 0xffu), b) + 16) >> 5;
-    } else {
-        const int ang = (int)(int8_t)(angw & 0xffu);
-        const int ia = ang_inv(angw);
-        const bool vert = mode >= 18;
-        const int ns = vert ? -1 : 1;
-        const int along = vert ? y : x, across = vert ? x : y;   // projection row / position on it
-        const int pa = __mul24(along + 1, ang);
-        const int idx = pa >> 5, fact = pa & 31;
-        const int nr0 = -1 - across - idx;                       // -(iIdx + across + 1)
-        const bool bflt = !P265R_HV_FAST && !PAIR && (mode == 26 || mode == 10);   // HV_FAST: copies above
-        const int k1 = ang_ref<2 * n>(nr0 - 1, ia, ns);          // computed unconditionally: a select, no branch
-        const int i1 = bflt ? (vert ? 2 * n - 1 - y : 2 * n + 1 + x) : k1;
-        const int a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(i1);
-        pred = (__mul24(32 - fact, a) + __mul24(fact, b) + 16) >> 5;   // = a when iFact = 0 (b then unused)
-        if (bflt) {                                              // modes 26 / 10, luma: boundary smoothing
-            const int edge = clip_pel(uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - uref(2 * n)) >> 1), maxv);
-            pred = (vert ? x : y) == 0 ? edge : pred;
         }
     }
     return pred;
@@ -679,34 +682,34 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
     constexpr uint32_t msk = (0xffffu >> (LOG2 + 1)) * 0x00010001u;
     auto ref = [&](int i) { return (uint32_t)__builtin_amdgcn_ds_bpermute(i << 2, (int)v); };
     auto uref = [&](int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); };
+    if (mode >= 2) {                                           // angular first: the most frequent path
+        if (TAB) {                                             // AngTab4 entry (modes 10 / 26 included: fact 0)
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), (int)v);
+            const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), (int)v);
+            return ((__umul24(angw >> 24, a) + __umul24((angw >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+        }
+        if (P265R_HV_FAST && (angw & 0xffu) == 0u)              // modes 10 / 26: a copy (no chroma smoothing)
+            return ref(mode >= 18 ? 2 * n + 1 + x : 2 * n - 1 - y);
+        const int ang = (int)(int8_t)(angw & 0xffu);
+        const int ia = ang_inv(angw);
+        const bool vert = mode >= 18;
+        const int ns = vert ? -1 : 1;
+        const int along = vert ? y : x, across = vert ? x : y;
+        const int pa = __mul24(along + 1, ang);
+        const int idx = pa >> 5, fact = pa & 31;
+        const int nr0 = -1 - across - idx;
+        const uint32_t a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(ang_ref<2 * n>(nr0 - 1, ia, ns));
+        return ((__umul24(32 - fact, a) + __umul24(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+    }
     if (mode == 0) {
         const uint32_t lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
         const uint32_t s = __umul24(n - 1 - x, lft) + __umul24(x + 1, uref(3 * n + 1)) + __umul24(n - 1 - y, top) +
                            __umul24(y + 1, uref(n - 1)) + rnd;
         return (s >> (LOG2 + 1)) & msk;
     }
-    if (mode == 1) {
-        const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
-        const uint32_t s = (uint32_t)wave_sum<false, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>(in ? (int)v : 0, 0) + rnd;
-        return (s >> (LOG2 + 1)) & msk;
-    }
-    if (TAB) {                                                 // AngTab4 entry (modes 10 / 26 included: fact 0)
-        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), (int)v);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), (int)v);
-        return ((__umul24(angw >> 24, a) + __umul24((angw >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
-    }
-    if (P265R_HV_FAST && (angw & 0xffu) == 0u)                  // modes 10 / 26: a copy (no chroma smoothing)
-        return ref(mode >= 18 ? 2 * n + 1 + x : 2 * n - 1 - y);
-    const int ang = (int)(int8_t)(angw & 0xffu);
-    const int ia = ang_inv(angw);
-    const bool vert = mode >= 18;
-    const int ns = vert ? -1 : 1;
-    const int along = vert ? y : x, across = vert ? x : y;
-    const int pa = __mul24(along + 1, ang);
-    const int idx = pa >> 5, fact = pa & 31;
-    const int nr0 = -1 - across - idx;
-    const uint32_t a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(ang_ref<2 * n>(nr0 - 1, ia, ns));
-    return ((__umul24(32 - fact, a) + __umul24(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+    const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
+    const uint32_t s = (uint32_t)wave_sum<false, (LOG2 == 2 ? 1 : (LOG2 == 3 ? 2 : 4))>(in ? (int)v : 0, 0) + rnd;
+    return (s >> (LOG2 + 1)) & msk;
 }
 
 // Clip1(pred + res) of both halves: pred packed (0..255 per half), res two int16 residuals
@@ -779,12 +782,14 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     } else {                                                     // all internal (q2 column, q0 corner, q1 row)
         v = bp(s <= 8 ? 91 - 8 * s : s + 19, rec);
     }
+    // only the first stage can find no reference available: stages 1-3 always have the region's earlier
+    // sub-blocks (q1: q0's column on the left, q2: q0's row above, q3: both) -- their none bits are 0
     if constexpr (CH) {
-        v = none ? 0x00800080 : v;
+        if constexpr (Q == 0) v = none ? 0x00800080 : v;
         const int rq = (int)cquad_recon(cpred<2, true>(mode, te, (uint32_t)v, xs, ys, lane), (uint32_t)r16);
         return qid == Q ? rq : rec;
     } else {
-        v = none ? 128 : v;
+        if constexpr (Q == 0) v = none ? 128 : v;
         const int rq = clip_pel(fast_pred<2, false, true>(mode, te, v, xs, ys, lane, lane, 0) + r16, maxv);
         return qid == Q ? rq : rec;
     }

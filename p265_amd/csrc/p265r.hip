@@ -52,6 +52,10 @@ using namespace p265r;
 #ifndef P265R_PHASE_ORDER
 #define P265R_PHASE_ORDER 0        // pipelined contexts: one intra phase at a time; residual + prep overlap loop filters
 #endif
+#ifndef P265R_SAO_AUX
+#define P265R_SAO_AUX 0            // pipelined chip-filling batches: prep on the lane stream, the loop filters on the
+                                   // lane's aux stream, so the next run's residual + prep overlap this run's SAO
+#endif
 #ifndef P265R_UP_STREAM
 #define P265R_UP_STREAM 0          // 0: a batch uploads on its own lane stream; 1: on an upload stream created with
                                    // the context; 2: created at the first upload (after the lanes)
@@ -140,7 +144,8 @@ struct p265r_ctx {
     // occupancy caps by dynamic-LDS padding of the SAO / residual launches (P265R_SAO_LDS /
     // P265R_RES_LDS bytes per block, experiments builds): fewer waves per CU streamed faster in the
     // HBM probe (tools/bw_probe.hip)
-    int sao_lds = 0, res_lds = 0;
+    int sao_lds = 0, res_lds = 0, prep_lds = 0;
+    int prep_last = 0;             // experiments: P265R_PREP_LAST=1 enqueues the prep kernel after the residual kernels
     int order_r = 1;               // P265R_ORDER_R=0 (experiments): ordered runs' residual phase waits only for its own batch  // lanes at the highest stream priority, prep streams at the lowest (P265R_STREAM_PRIO)
     int pipe_waves = 8;        // row pipeline waves per workgroup while other lanes have work (experiments:
                                // P265R_PIPE_WAVES 4, 6, 8)
@@ -197,6 +202,8 @@ struct p265r_batch {
     bool ragged = false;       // some picture is smaller than the context size (Geo::ragged)
     std::vector<std::array<int, 2>> size;   // per picture: luma width, height
     int runs = 0;              // p265r_batch_run calls so far
+    hipEvent_t sao_done = nullptr;     // P265R_SAO_AUX: recorded on the aux stream after a run's loop filters
+    bool sao_pending = false;          // ... and not yet joined into the lane stream (join_sao)
     hipEvent_t intra_done = nullptr;   // recorded after each run's intra phase (the last reader of the
                                        // residual pool and job lists): the next run's residual + prep
                                        // phase waits for it instead of for the whole previous run
@@ -342,6 +349,15 @@ void rows_diag(hipStream_t st, const int* dbg, int grid, int W) {
 }
 #endif
 
+// P265R_SAO_AUX: order the batch's lane stream after its last run's loop filters (host-facing reads)
+int join_sao(p265r_batch* b) {
+    if (b->sao_pending) {
+        HIP_TRY(hipStreamWaitEvent(b->stream, b->sao_done, 0));
+        b->sao_pending = false;
+    }
+    return P265R_OK;
+}
+
 template <int W, int WPE>
 int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     Geo g = ctx->geo;
@@ -416,6 +432,8 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     }
     if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 4) return launch_rows_w<4, 1>(ctx, b, st, alone);
     if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 6) return launch_rows_w<6, 1>(ctx, b, st, alone);
+    if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 10 && !(ctx->split && 2 * (long long)b->n_pics <= ctx->num_cus))
+        return launch_rows_w<10, 5>(ctx, b, st, alone);
     if (ctx->lean == 0 && (ctx->row_waves == 8 || (ctx->row_waves == 0 && !alone))) return launch_rows_w<8, 1>(ctx, b, st, alone);
 #endif
     // a batch small enough for the component split with one workgroup per CU (the latency regime:
@@ -515,14 +533,16 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("P265R_PIPE_WAVES")) {
         const int w = std::atoi(v);
-        if (w == 4 || w == 6 || w == 8) ctx->pipe_waves = w;
+        if (w == 4 || w == 6 || w == 8 || w == 10) ctx->pipe_waves = w;
     }
     if (const char* v = std::getenv("P265R_STREAM_PRIO")) ctx->stream_prio = std::atoi(v) != 0;
-    for (const char* k : {"P265R_SAO_LDS", "P265R_RES_LDS"})
+    for (const char* k : {"P265R_SAO_LDS", "P265R_RES_LDS", "P265R_PREP_LDS", "P265R_PREP_LAST"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_ORDER_R")) ctx->order_r = std::atoi(v) != 0;
     if (const char* v = std::getenv("P265R_SAO_LDS")) ctx->sao_lds = std::min(65536, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("P265R_RES_LDS")) ctx->res_lds = std::min(32768, std::max(0, std::atoi(v)));
+    if (const char* v = std::getenv("P265R_PREP_LDS")) ctx->prep_lds = std::min(65536, std::max(0, std::atoi(v)));
+    if (const char* v = std::getenv("P265R_PREP_LAST")) ctx->prep_last = std::atoi(v) != 0;
 #endif
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -925,7 +945,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // * otherwise (a lone lane's re-runs) the EARLY residual phase: residual + prep start when this
     //   batch's previous intra phase ends, beside its previous loop filters.
     const bool big = b->n_pics >= ctx->num_cus;
-    const int fork_prep = big ? ctx->fork_prep : 0;
+    // P265R_SAO_AUX: the loop filters of this run go to the lane's aux stream (after its intra phase), the
+    // prep kernel stays on the lane, so the next run's residual + prep phase overlaps this run's loop filters
+    const bool sao_aux = P265R_SAO_AUX && !P265R_PHASE_ORDER && !P265R_EARLY_RESIDUAL && ctx->pipeline > 1 && big && prep &&
+                         !ctx->timing && ctx->fork_prep == 1 && (b->sao || b->dbk) && !(skip & 4);
+    const int fork_prep = big && !sao_aux ? ctx->fork_prep : 0;
     const bool ordered = P265R_PHASE_ORDER && ctx->pipeline > 1 && prep && fork_prep == 1 && !ctx->timing;
     const bool early = !ordered && P265R_EARLY_RESIDUAL && prep && fork_prep == 1 && !ctx->timing && b->intra_done &&
                        !(skip & 1);
@@ -973,14 +997,16 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
             HIP_TRY(hipStreamWaitEvent(ps, ctx->fork_ev[li], 0));
         }
     }
-    if (prep) {
+    auto launch_prep = [&]() -> int {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
         // of the residuals, timed with the residual phase; enqueued first so that, forked, its
         // waves start before the residual kernels fill the chip
-        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, 0, ps>>>(b->d_pics, g, b->view);
+        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, ctx->prep_lds, ps>>>(b->d_pics, g, b->view);
         ++tm.residual_launches;
         if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[fork_prep == 2 ? 0 : (size_t)b->lane], ps));
-    }
+        return P265R_OK;
+    };
+    if (prep && !ctx->prep_last) { int rc = launch_prep(); if (rc) return rc; }
     if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
         residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
         ++tm.residual_launches;
@@ -1005,6 +1031,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
         ++tm.residual_launches;
     }
+    if (prep && ctx->prep_last) { int rc = launch_prep(); if (rc) return rc; }
     if (prep && ps != s) HIP_TRY(hipStreamWaitEvent(s, ctx->join_ev[fork_prep == 2 ? 0 : (size_t)b->lane], 0));
     if (rs != s) {
         HIP_TRY(hipEventRecord(ctx->join2_ev[(size_t)b->lane], rs));
@@ -1023,6 +1050,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         // per-CU workgroup slots cleared per run; the error word (d_err[0]) is sticky from upload on,
         // so p265r_batch_status / p265r_batch_download report a give-up in ANY run of the batch
         HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16, s));
+        // the previous run's loop filters (on the aux stream) read the planes this run writes
+        if (b->sao_pending) { HIP_TRY(hipStreamWaitEvent(s, b->sao_done, 0)); b->sao_pending = false; }
         if (ordered && ctx->last_lf_valid) HIP_TRY(hipStreamWaitEvent(s, ctx->last_lf_ev, 0));
         // does another lane have a run enqueued that the API has not synchronised since?  (host
         // state only, so the build a run gets is a function of the call sequence)
@@ -1056,6 +1085,21 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (ctx->debug_sync) { fprintf(stderr, "[p265r] intra phase enqueued\n"); HIP_TRY(hipStreamSynchronize(s)); fprintf(stderr, "[p265r] intra phase done\n"); }
     if (ctx->timing) HIP_TRY(hipEventRecord(ev[2], s));
     // ---- in-loop filters: deblocking + SAO ----------------------------------------------
+    const hipStream_t lane_s = s;
+    if (sao_aux) {
+        const size_t li = (size_t)b->lane;
+        if (ctx->aux.size() <= li) {
+            ctx->aux.resize(li + 1, nullptr); ctx->fork_ev.resize(li + 1, nullptr); ctx->join_ev.resize(li + 1, nullptr);
+        }
+        if (!ctx->aux[li]) {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->aux[li], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->fork_ev[li], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->join_ev[li], hipEventDisableTiming));
+        }
+        if (!b->sao_done) HIP_TRY(hipEventCreateWithFlags(&b->sao_done, hipEventDisableTiming));
+        s = ctx->aux[li];
+        HIP_TRY(hipStreamWaitEvent(s, b->intra_done, 0));
+    }
     if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && g.h % 8 == 0 && !(skip & 4)) {
         // SAO only, CTB 32 / 64: the 16-samples-per-lane strip kernel (sao_strip16.h), one wave per
         // (picture, CTB row, component, 992-sample strip), 4 waves per block, blocks dealt XCD-aware;
@@ -1093,6 +1137,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
     }
+    if (sao_aux) {
+        HIP_TRY(hipEventRecord(b->sao_done, s));
+        b->sao_pending = true;
+        s = lane_s;
+    }
     if (ordered) {                                   // the next batch's intra phase starts after this
         if (!ctx->last_lf_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->last_lf_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(ctx->last_lf_ev, s));
@@ -1112,6 +1161,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
 int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pics, int n_pics) {
     if (!ctx || !b || !pics || n_pics != b->n_pics) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = join_sao(b)) return rc;
     const Geo& g = ctx->geo;
     // planes to copy: (host destination, device source, row pitch, width, height)
     struct Item { void* dst; const unsigned char* src; int pitch, w, h; size_t bytes; };
@@ -1182,6 +1232,7 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
 int p265r_batch_status(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = join_sao(b)) return rc;
     HIP_TRY(hipStreamSynchronize(b->stream));
     // the lane is idle now (every run on it, of any batch, has completed)
     ctx->lane_busy &= ~(1u << b->lane);
@@ -1197,6 +1248,7 @@ int p265r_batch_status(p265r_ctx* ctx, p265r_batch* b) {
 int p265r_batch_digest(p265r_ctx* ctx, p265r_batch* b, int which, uint64_t* out, int n) {
     if (!ctx || !b || !out || n != 3 * b->n_pics || (which != 0 && which != 1)) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = join_sao(b)) return rc;
     // after every run enqueued on the batch's lane (stream order); one device buffer per call
     unsigned long long* d = nullptr;
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), sizeof(uint64_t) * (size_t)n));
@@ -1231,11 +1283,13 @@ int p265r_batch_job_count(p265r_ctx* ctx, p265r_batch* b, uint64_t* luma, uint64
 int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     if (!ctx || !b) return P265R_EINVAL;
     (void)hipSetDevice(ctx->device);
+    (void)join_sao(b);
     if (ctx->pending == b) ctx->pending = nullptr;
     // its lane may still run it: the allocation is reused by the next upload (another stream); the
     // lane stream's last run waited for every residual / prep kernel of the batch
     hipError_t e = b->stream ? hipStreamSynchronize(b->stream) : hipSuccess;
     if (b->intra_done) (void)hipEventDestroy(b->intra_done);
+    if (b->sao_done) (void)hipEventDestroy(b->sao_done);
     if (b->mem) {
         // keep the larger of (cache, this allocation) for the next upload (its runs are complete)
         if (!ctx->cache_mem || b->bytes > ctx->cache_bytes) {
