@@ -382,7 +382,21 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     auto absorbed_mask = [](unsigned long long H, unsigned long long Hp) {
         return (H << 1) | (H << 2) | (H << 3) | (Hp >> 63) | (Hp >> 62) | (Hp >> 61);
     };
-    int c_out = 0;
+    // does a job read the row above the CTU beyond the CTU's own columns (the top-right CTU's bottom row)?
+    // Then the row kernel must wait for that CTU before running it; every job before the first such one
+    // runs after the CTU above alone (intra_rows.h: the top-right wait moves into the CTU).  A TB at CTB
+    // position (xr, 0) reads top samples up to x = xr + 2n - 1; a quad's second sub-block up to X + 11.
+    // Only when the top-right CTU is usable (same slice and tile, inside the picture: flags bit 3)
+    auto needs_tr = [&](uint32_t w0, bool quad, bool chroma) -> bool {
+        const uint32_t o = (w0 & 0x1fffu) - (chroma ? 4096u : 0u);
+        const int xr = (int)(o & (chroma ? 31u : 63u)), yr = (int)(o >> (chroma ? 5 : 6));
+        const int reach = quad ? xr + 12 : xr + (8 << ((w0 >> 13) & 3u));
+        return (yr == 0) & (reach > (chroma ? ctb >> 1 : ctb)) & ((flags & 8u) != 0u);
+    };
+    auto first_of = [&](unsigned long long m, unsigned long long me, int out) {   // index of m's first job
+        return m ? out + (int)__popcll(me & ((1ull << (__ffsll((long long)m) - 1)) - 1ull)) : -1;
+    };
+    int c_out = 0, tr_c = -1;
     unsigned long long hp = 0;
     for (int base = 0; base < n_chroma; base += 64) {
         const int s = base + lane;
@@ -405,9 +419,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32;
         }
         if (emit) prep_job_store(jobs + c_out + rank(me_), J);
+        if (tr_c < 0) tr_c = first_of(__ballot(emit && needs_tr(J.w[0], hd, true)), me_, c_out);
         c_out += __popcll(me_);
     }
-    int n_out = 0;
+    int n_out = 0, tr_l = -1;
     hp = 0;
     for (int base = 0; base < n_luma; base += 64) {
         const int s = base + lane;
@@ -423,9 +438,16 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const uint32_t w1 = job_w1(l.w0, l.w5, angv);
         const IntraJob J = hd ? make_quad(sj + sq, qb, qc) : luma_job(l, P.zero_off, w1);
         if (emit) prep_job_store(jobs + c_out + n_out + rank(me_), J);
+        if (tr_l < 0) tr_l = first_of(__ballot(emit && needs_tr(J.w[0], hd, false)), me_, n_out);
         n_out += __popcll(me_);
     }
-    if (lane == 0) *(__attribute__((address_space(1))) uint32_t*)(P.jcount + addr) = (uint32_t)n_out | (uint32_t)c_out << 16;
+    // per CTU: job counts (luma | chroma << 16) and the index of the first job that reads the top-right
+    // CTU in each list (= the count when none does)
+    if (lane == 0) {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        *(__attribute__((address_space(1))) u2*)(P.jcount + 2 * addr) =
+            u2{(uint32_t)n_out | (uint32_t)c_out << 16, (uint32_t)(tr_l < 0 ? n_out : tr_l) | (uint32_t)(tr_c < 0 ? c_out : tr_c) << 16};
+    }
 }
 
 }  // namespace p265r

@@ -155,19 +155,27 @@ __device__ __forceinline__ uint32_t angtab_entry(int m, int p) {
     return a | b << 8 | (uint32_t)fact << 16 | (uint32_t)(32 - fact) << 24;
 }
 
-struct WaveLds {                 // one wave's private CTU state (4432 B): a wave holds one row
+struct WaveLds {                 // one wave's private CTU state (4564 B): a wave holds one row
     uint8_t  ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
     union {                      // ref: raw / final linear reference arrays (8-bit samples)
         struct {
             uint8_t y[64 * 64];          // interior luma, stride 64
             uint8_t yleft[64];           // right column of the previous CTU of this row
+            uint8_t ytop[132];           // XG: the row above, [4 + x] for x = -4 .. 2 CTB - 1
         };
         struct {
             uint8_t c[2][32 * 32];       // interior chroma, stride 32
             uint8_t cleft[2][32];
+            uint8_t ctop[2][68];         // XG: per plane as ytop
         };
     };
 };
+#ifndef P265R_TR_SEG
+#define P265R_TR_SEG 0                   // 1: the job loop in two segments around the top-right wait
+#endif
+#ifndef P265R_TR_DEFER
+#define P265R_TR_DEFER 1                 // 0: wait for the top-right CTU before the CTU starts (A/B knob)
+#endif
 // job word w0 addresses a TB origin as yr * 64 + xr (luma) or 4096 + yr * 32 + xr (chroma,
 // intra_prep.h); WaveLds byte of that origin = w0 offset + kOrg[chroma]
 constexpr uint32_t kOrgL = offsetof(WaveLds, y);
@@ -862,14 +870,28 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
 // (≈100 VGPRs) for a batch that runs alone, and register-lean (WPE 6: 80 VGPRs, a few spills)
 // for batches overlapping other batches' residual / loop-filter kernels, whose waves then
 // fit beside it on every SIMD (p265r.hip launch_rows; measured in DESIGN.md §6).
-template <int W, int WPE>
+//
+// XG (cross-group chains, the latency regime): every picture's luma chain and chroma chain each run on
+// `xg` workgroups of W waves (W = 4: one wave per SIMD, on xg CUs), rows dealt statically (wave k of the
+// chain's xg * W runs rows k, k + xg W, ...); row progress and the rows' bottom lines live in global
+// memory (XgBuf), read and written with agent-scope atomics (coherent across the XCDs' L2s), and a
+// CTU's row above is copied from there into the wave's ytop / ctop.  One line per CTU row (no parity
+// reuse): a CTU's publish never waits for the row below to have read the line.
+struct XgBuf {
+    int* prog;                   // [pic][comp][row]: seq << 16 | CTUs done
+    uint8_t* lines;              // [pic][comp][row][(wc + 2) * CTB]: the row's bottom samples at + CTB
+                                 // (chroma: Cb at + CTB / 2, Cr (wc + 2) * CTB / 2 further)
+    int xg, seq;                 // workgroups per chain; this run's tag
+};
+
+template <int W, int WPE, bool XG = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
 void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
                                                            const int16_t* __restrict__ resid,
                                                            Geo g, int n_pics, int fs_count, int lead,
                                                            int* __restrict__ err_flag,
-                                                           int* __restrict__ dbg, int split) {
+                                                           int* __restrict__ dbg, int split, XgBuf xb) {
     // debug trace (P265R_DEBUG_DIAG builds, P265R_DEBUG_SYNC=1): host-mapped words, one per wave
 #if defined(P265R_DEBUG_DIAG) && !defined(P265R_DBG_NOTRACE)
 #define P265R_TRACE(code) do { if (dbg && lane == 0) __hip_atomic_store(dbg + blockIdx.x * W + wave, (code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
@@ -918,7 +940,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     const int b = split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
     const int split_comp = (int)(blockIdx.x & 1u);
     const int n_my = b < n_pics ? (n_pics - b + G - 1) / G : 0;
-    const int rows_total = n_my * units;
+    const int rows_total = XG ? g.hc : n_my * units;
+    // XG: this workgroup's chain (picture, component) and its first wave's index in the chain
+    const int xg_chain = XG ? (int)blockIdx.x / xb.xg : 0;
+    const int xg_wave = XG ? ((int)blockIdx.x - xg_chain * xb.xg) * W + wave : 0;
+    const size_t xg_row_bytes = (size_t)(g.wc + 2) << g.ctb_log2;
     const int ctb = 1 << g.ctb_log2;
     // bounded spin-wait on an LDS word; false = gave up (error published, caller bails out).
     // Every condition is made wave-uniform (readfirstlane) so the loops are scalar loops.
@@ -936,8 +962,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         for (int spins = 0; spins < (1 << 24); ++spins) {
             if (spins == 0 && __builtin_amdgcn_readfirstlane((int)ready())) return true;
             if (__builtin_amdgcn_readfirstlane((int)ready())) { P265R_WAIT_ADD; return true; }
-            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-                return false;
+            if (__builtin_amdgcn_readfirstlane(XG ? __hip_atomic_load(gptr(err_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                  : __hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                return false;                               // (XG: any chain's failure ends every wait)
             __builtin_amdgcn_s_sleep(P265R_SPIN_SLEEP);   // 64 cycles per unit; each poll costs issue slots
         }
         __hip_atomic_store(&ctl.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // all lanes, same value
@@ -947,14 +974,21 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     bool failed = false;
 
     P265R_TRACE(1);
+    int xg_next = xg_wave;                                 // XG: this wave's next row
     for (;;) {
         // row queue: the whole wave executes the atomic (no lane-0 branch inside the loop);
         // only lane 0 contributes, so the wave takes exactly one row
-        int r = __hip_atomic_fetch_add(&ctl.next_row, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int r;
+        if constexpr (XG) {
+            r = xg_next;
+            xg_next += xb.xg * W;
+        } else {
+            r = __hip_atomic_fetch_add(&ctl.next_row, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         r = __builtin_amdgcn_readfirstlane(r);
         if (r >= rows_total || failed) break;
         P265R_TRACE(2 | (r << 8));
-        if (g.fair) {
+        if (!XG && g.fair) {
             // publish the rows this workgroup has dequeued; priority 1 while behind the partner
             const int key = __builtin_amdgcn_readfirstlane(ctl.cu_slot), rank = __builtin_amdgcn_readfirstlane(ctl.cu_rank);
             RowCuSlot* cs = reinterpret_cast<RowCuSlot*>(err_flag + 64) + key;
@@ -969,7 +1003,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         // L0 .. L(d-1), then L(d) C0 L(d+1) C1 ..., then the remaining chroma rows.  Either
         // chain's rows stay in order, so a dequeued row's predecessor is always held by a wave.
         int cy, comp;                                      // comp 0: luma chain, 1: chroma (Cb + Cr)
-        if (split) {
+        if (XG) {
+            cy = r; comp = xg_chain & 1;
+        } else if (split) {
             cy = rem; comp = split_comp;
         } else {
             const int d = min(lead, g.hc);
@@ -982,7 +1018,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             }
         }
         const int slot = j % fs_count, gen = j / fs_count;
-        const DevPic* Pp = pics + b + j * G;
+        const DevPic* Pp = XG ? pics + (xg_chain >> 1) : pics + b + j * G;
         const p265r_ctu* ctus = uniform(gload(&Pp->ctus));
         const IntraJob* jobs = uniform(gload(&Pp->jobs));
         const uint32_t* jcount = uniform(gload(&Pp->jcount));
@@ -997,7 +1033,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         // picture slot reuse: every row of picture j waits until picture j - fs_count (the
         // slot's previous occupant) has completed all its rows; those rows were dequeued
         // earlier and are held by running waves, so this wait always ends.
-        if (!wait_until([&] {
+        if (!XG && !wait_until([&] {
                 return __hip_atomic_load(&ctl.done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= gen * units;
             })) { failed = true; break; }
         P265R_TRACE(3 | (r << 8));
@@ -1009,16 +1045,26 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         const unsigned char* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
         int* my_prog = &prog[(slot * g.hc + cy) * 2 + comp];
         const int* up_prog = &prog[(slot * g.hc + (cy > 0 ? cy - 1 : 0)) * 2 + comp];
-        const int tag = (j & 0xffff) << 16;
-        __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int tag = ((XG ? xb.seq : j) & 0xffff) << 16;
+        // XG: this chain's progress words and lines (global)
+        P265R_GLOBAL int* xg_prog = XG ? gptr_w(xb.prog) + (size_t)xg_chain * g.hc : nullptr;
+        P265R_GLOBAL uint8_t* xg_line = XG ? gptr_w(xb.lines) + (size_t)xg_chain * g.hc * xg_row_bytes : nullptr;
+        if constexpr (XG) {
+            if (lane == 0) __hip_atomic_store(xg_prog + cy, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(my_prog, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
 
         // CTU header (first TB index | job counts) loaded one CTU ahead, and the next CTU's first
         // 64 job records loaded right after this CTU's last job: a CTU then starts with its
         // records in registers (one dependent round trip, its first residual, instead of three)
+        // (jcount: two words per CTU -- the job counts and the index of each list's first job that
+        // reads the top-right CTU, intra_prep.h)
         auto hdr_load = [&](int a) {
-            return make_uint2(gload(reinterpret_cast<const uint2*>(ctus + a)).x, *gptr(jcount + a));
+            const uint2 jp = gload(reinterpret_cast<const uint2*>(jcount + 2 * a));
+            return make_uint4(gload(reinterpret_cast<const uint2*>(ctus + a)).x, jp.x, jp.y, 0u);
         };
-        uint2 hdr_n = hdr_load(cy * pwc);
+        uint4 hdr_n = hdr_load(cy * pwc);
 #ifndef P265R_ROW_PRIO
 #define P265R_ROW_PRIO 3
 #endif
@@ -1038,29 +1084,59 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         uint2 rec1 = make_uint2(0, 0);
         bool pre = false;                                  // rec0 / rec1 hold this CTU's first records
         for (int cx = 0; cx < pwc; ++cx) {
-            // ---- wait for the row above (2-CTU lag) -------------------------------------
-            if (cy > 0) {
-                const int need = min(cx + 2, pwc);
-                if (!wait_until([&] {
-                        const int v = __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        return (v & 0xffff0000) == tag && (v & 0xffff) >= need;
-                    })) { failed = true; break; }
-            }
-            P265R_TRACE(4 | (cx << 8) | (r << 16));
+            // ---- wait for the row above -------------------------------------------------
+            // The CTU above (1-CTU lag) before the CTU starts; the top-right CTU (2-CTU lag) before the
+            // first job that reads it (prep: per CTU and chain, `tr`) and, read or not, before this CTU's
+            // bottom row goes into the line buffer: that overwrites the row above the CTU for the row
+            // below the one above, which reads it up to its CTU cx + 1 (the corner)
             const int x0 = cx << g.ctb_log2, y0 = cy << g.ctb_log2;
             const int addr = cy * pwc + cx;
             // this CTU's job list (intra_prep_kernel): first job = its first TB index; job counts:
             // luma in bits 0..15, chroma (listed first) in bits 16..31 (intra_prep.h)
             const uint32_t tb_begin = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
             const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
+            const uint32_t trw = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.z);
             if (cx + 1 < pwc) hdr_n = hdr_load(addr + 1);    // in flight during this CTU
             const int n_chroma = (int)(jc >> 16);
             const int nt = comp ? n_chroma : (int)(jc & 0xffffu);
+            // (deferred only in the latency layouts -- XG and the W = 16 split: the throughput builds keep the
+            // 2-CTU-lag start, whose job loop has no per-job test; measured: pipelined step 1.7 % slower with it)
+            constexpr bool kDefer = P265R_TR_DEFER && (XG || W == 16);
+            const int tr = !kDefer ? 0 : comp ? (int)(trw >> 16) : (int)(trw & 0xffffu);   // first job reading the top-right CTU
+            const bool tr_ctu = cy > 0 && cx + 1 < pwc;        // a top-right CTU exists (else nothing to wait for)
+            auto up_ready = [&](int need) {
+                const int v = XG ? __hip_atomic_load(xg_prog + (cy - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return (v & 0xffff0000) == tag && (v & 0xffff) >= need;
+            };
+            // XG: the row above's line, x in [x0 + 4 k0 - 4, x0 + 4 k1 - 4) (component units), into ytop /
+            // ctop [4 k0, 4 k1): one dword per lane (chroma: lanes 0-31 Cb, 32-63 Cr), agent-scope loads
+            // after the progress word that covers them (the writer completed them before storing it)
+            const int cts = ctb >> comp;
+            auto xg_copy = [&](int k0, int k1) {
+                const int h = comp ? lane >> 5 : 0, k = k0 + (comp ? lane & 31 : lane);
+                if (k < k1) {
+                    const P265R_GLOBAL uint8_t* src = xg_line + (size_t)(cy - 1) * xg_row_bytes +
+                                                      (size_t)h * (xg_row_bytes >> 1) + cts + (x0 >> comp) - 4 + 4 * k;
+                    const uint32_t v = __hip_atomic_load(reinterpret_cast<const P265R_GLOBAL uint32_t*>(src),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uint8_t* dst = comp ? &L.ctop[h][4 * k] : &L.ytop[4 * k];
+                    *reinterpret_cast<uint32_t*>(dst) = v;
+                }
+                wave_sync();
+            };
+            auto wait_up = [&](int need) { return wait_until([&] { return up_ready(need); }); };
+            const bool early = tr_ctu && tr == 0;               // the first job already reads the top-right CTU
+            bool tr_done = !tr_ctu || early;                    // waited for the top-right CTU
+            if (cy > 0 && !wait_up(early || !tr_ctu ? min(cx + 2, pwc) : cx + 1)) { failed = true; break; }
+            if (XG && cy > 0) xg_copy(0, (early ? 2 * cts : cts) / 4 + 1);
+            P265R_TRACE(4 | (cx << 8) | (r << 16));
             const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
-            // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr)
-            const uint8_t* ltop_l = line_up + x0;
-            const uint8_t* ltop_c = line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
-            const uint8_t* ltop_cb = line_up + g.w + (x0 >> 1);
+            // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr); XG: the wave's copy
+            const uint8_t* ltop_l = XG ? &L.ytop[4] : line_up + x0;
+            const uint8_t* ltop_c = XG ? &L.ctop[lane >> 5][4] : line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
+            const uint8_t* ltop_cb = XG ? &L.ctop[0][4] : line_up + g.w + (x0 >> 1);
+            const uint32_t cr_off = XG ? (uint32_t)sizeof(L.ctop[0]) : (uint32_t)g.cw;   // Cb -> Cr in the row above
 
             // residual of job t: two aligned 16-B loads per lane (fixed shape, pools padded
             // by 64 B), issued while job t-1 is processed.  TB offsets are multiples of 16.
@@ -1133,7 +1209,28 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #ifdef P265R_JOB_UNROLL
 #pragma unroll P265R_JOB_UNROLL
 #endif
+            // the top-right wait before job tr (the row above the CTU suffices for the jobs before it)
+#if P265R_TR_SEG
+            // two segments: jobs [0, tr), the top-right wait, jobs [tr, nt) (no per-job test)
+            int t = 0;
+#pragma unroll 1
+            for (int seg = tr_done || tr >= nt ? 1 : 0; seg < 2; ++seg) {
+            if (seg == 1 && !tr_done) {
+                if (!wait_up(cx + 2)) { failed = true; break; }
+                if (XG) xg_copy(cts / 4 + 1, 2 * cts / 4 + 1);
+                tr_done = true;
+            }
+            const int t_end = seg == 0 ? tr : nt;
+            for (; t < t_end; ++t) {
+#else
+            const int t_trw = tr_done || tr >= nt ? -1 : tr;
             for (int t = 0; t < nt; ++t) {
+                if (t == t_trw) {                       // (a failed wait runs on; the loop exits after the job)
+                    failed = !wait_up(cx + 2);
+                    if (XG) xg_copy(cts / 4 + 1, 2 * cts / 4 + 1);
+                    tr_done = true;
+                }
+#endif
 #ifdef P265R_JOB_STATS
                 const long long tj0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1184,14 +1281,14 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
                 const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
                 if (w5 & J5_QUAD) {
-                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tcb, (uint32_t)g.cw, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
+                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tcb, cr_off, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
                     else recon_quad<false>(lbase, tl, 0u, w0, w1, w2, tab, c16, ln);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
                         case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;
                         case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;
                         case 2: recon_fast16(lbase, tl, w0, w1, w5, make_uint4((uint32_t)c16, (uint32_t)c16m, 0u, 0u), ln); break;
-                        case 5: recon_cfast8(lbase, tcb, (uint32_t)g.cw, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, tab); break;
+                        case 5: recon_cfast8(lbase, tcb, cr_off, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, tab); break;
                         default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln, tab); break;
                     }
                 } else {
@@ -1219,6 +1316,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 }
 #endif
             }
+#if P265R_TR_SEG
+            }
+#endif
+            if (failed) break;                             // (wait_until published the error)
+            // before this CTU's bottom row goes into the line buffer (whether or not a job read it; XG:
+            // one line per row, nothing to overwrite)
+            if (!XG && !tr_done && !wait_up(cx + 2)) { failed = true; break; }
 
             if (cx + 1 < pwc) {                            // the next CTU's first 64 job records
                 const uint32_t tb2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
@@ -1267,12 +1371,27 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                                 *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
                     }
                 }
-                unsigned char* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
-                if (lane < wv) lc[lane] = src[(hv - 1) * ist + lane];
+                if constexpr (XG) {                            // bottom row, whole dwords (past the edge: unread)
+                    P265R_GLOBAL uint8_t* dl = xg_line + (size_t)cy * xg_row_bytes + (c == 2 ? xg_row_bytes >> 1 : 0) + cs + xb;
+                    if (lane < cs / 4)
+                        __hip_atomic_store(reinterpret_cast<P265R_GLOBAL uint32_t*>(dl) + lane,
+                                           *reinterpret_cast<const uint32_t*>(src + (hv - 1) * ist + 4 * lane),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    unsigned char* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
+                    if (lane < wv) lc[lane] = src[(hv - 1) * ist + lane];
+                }
                 uint8_t* lf = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
                 if (lane < hv) lf[lane] = src[lane * ist + wv - 1];
             }
-            __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if constexpr (XG) {
+                // the line's stores complete (at the agent's coherence point) before the progress word
+                // that announces them; the plane stores are read only by later kernels
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(xg_prog + cy, tag | (cx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             wave_sync();
         }
         if (failed) break;

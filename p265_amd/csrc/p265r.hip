@@ -134,7 +134,9 @@ struct p265r_ctx {
     int skip = 0;              // P265R_SKIP (timing experiments on batch re-runs, p265r_batch_run)
     int lean = 1;              // experiments: W = 8 row kernel build 0 unconstrained (P265R_LEAN=0), 1 register-lean
     int split = 1;             // component split of small batches (P265R_SPLIT=0: off; launch_rows_w)
+    int xg = 4;                // workgroups per chain of the cross-group row kernel (P265R_XG; 0: off; launch_rows)
     bool last_split = false;   // the last row-kernel launch was split (p265r_describe)
+    bool last_xg = false;      // ... was the cross-group kernel
     int luma_lead = -1;        // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD);
                                // -1 = by run: 8 for a batch alone, 5 beside other lanes' batches (round 3,
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
@@ -200,6 +202,8 @@ struct p265r_batch {
     bool dbk = false;          // some CTU of the batch has deblocking on
     bool recon_input = false;  // P265R_PIC_RECON_INPUT: only the in-loop filters run
     bool ragged = false;       // some picture is smaller than the context size (Geo::ragged)
+    int* d_xg_prog = nullptr;  // cross-group row kernel (intra_rows.h XgBuf): progress words (zeroed per run
+    uint8_t* d_xg_lines = nullptr;  // with the CU slots), the rows' bottom lines; null: batch too large
     std::vector<std::array<int, 2>> size;   // per picture: luma width, height
     int runs = 0;              // p265r_batch_run calls so far
     hipEvent_t sao_done = nullptr;     // P265R_SAO_AUX: recorded on the aux stream after a run's loop filters
@@ -358,7 +362,7 @@ int join_sao(p265r_batch* b) {
     return P265R_OK;
 }
 
-template <int W, int WPE>
+template <int W, int WPE, bool XG = false>
 int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     Geo g = ctx->geo;
     // picture slots: the W rows in flight are consecutive in the queue, so they span at
@@ -370,7 +374,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
                kAngTabBytes;
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
-    auto fn = intra_rows_kernel<W, WPE>;
+    auto fn = intra_rows_kernel<W, WPE, XG>;
     bool split = false;
     {
         // every workgroup resident at once and holding a single picture: one slot is enough
@@ -384,6 +388,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
         // (on different CUs) when all of them fit at once -- the latency regime of a few large
         // pictures / tile units, where one workgroup's W waves on one CU bound the picture's time
         split = ctx->split && pc1 >= 1 && 2 * (long long)b->n_pics <= (long long)pc1 * ctx->num_cus;
+        if (XG) { fs = 1; split = true; }
     }
     const size_t lds = lds_of(fs);
     if (lds > 160 * 1024) return P265R_EUNSUPPORTED;
@@ -391,11 +396,13 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds));
     if (per_cu < 1) return P265R_EUNSUPPORTED;
-    const int grid = split ? 2 * b->n_pics : std::min(b->n_pics, per_cu * ctx->num_cus);
+    const int grid = XG ? 2 * b->n_pics * ctx->xg : split ? 2 * b->n_pics : std::min(b->n_pics, per_cu * ctx->num_cus);
     // fair CU sharing pairs the two workgroups of a CU (rank = arrival order & 1): only valid
     // when exactly two fit per CU and all of them are resident for the whole launch (grid <= 2
     // per CU, no workgroup starts after another ends) -- and only worth it for a batch alone
     g.fair = g.fair && alone && per_cu == 2 && !split;
+    // (XG: the progress words were cleared with the CU slots this run, so one tag serves every run)
+    const XgBuf xb{XG ? b->d_xg_prog : nullptr, XG ? b->d_xg_lines : nullptr, XG ? ctx->xg : 0, 1};
     g.ragged = b->ragged ? 1 : 0;
     int* dbg = nullptr;
 #ifdef P265R_DEBUG_DIAG
@@ -406,8 +413,9 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     }
 #endif
     const int lead = ctx->luma_lead >= 0 ? ctx->luma_lead : (alone ? 8 : 5);
-    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, lead, b->d_err, dbg, split ? 1 : 0);
+    fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, lead, b->d_err, dbg, split ? 1 : 0, xb);
     ctx->last_split = split;
+    ctx->last_xg = XG;
     HIP_TRY(hipGetLastError());
 #ifdef P265R_DEBUG_DIAG
     if (dbg) {
@@ -440,6 +448,9 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     // tile units, the decoder's small batches): W = 16, so every CTU row of a picture's chain can
     // be in flight at once (a 2-CTU-lag wavefront of 17 rows needs 17 waves; with 12 the rows
     // after the 12th wait for a whole row to finish)
+    // smaller still (every chain on xg CUs of its own): the cross-group kernel, one wave per SIMD
+    if (ctx->row_waves == 0 && b->d_xg_prog && 2 * (long long)b->n_pics * ctx->xg <= ctx->num_cus)
+        return launch_rows_w<4, 1, true>(ctx, b, st, alone);
     if (ctx->row_waves == 0 && ctx->split && P265R_SPLIT_W16 && 2 * (long long)b->n_pics <= ctx->num_cus)
         return launch_rows_w<16, 4>(ctx, b, st, alone);
     const int w = ctx->row_waves ? ctx->row_waves : (alone ? 12 : 8);
@@ -510,12 +521,13 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     ctx->n_ctus = g.wc * g.hc;
     // test knobs of the GPU parity matrix (bench.py refuses to run with any P265R_* variable set)
     for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_SAO_ROWS", "P265R_LUMA_LEAD", "P265R_ROW_WAVES",
-                          "P265R_FORK_PREP", "P265R_SPLIT"})
+                          "P265R_FORK_PREP", "P265R_SPLIT", "P265R_XG"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';
+    if (const char* v = std::getenv("P265R_XG")) { const int x = std::atoi(v); ctx->xg = (x == 2 || x == 4 || x == 8) ? x : 0; }
     if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::atoi(v) != 0 ? 1 : 0;
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {
         const int w = std::atoi(v);
@@ -680,7 +692,13 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     size_t off = 0;
     const size_t o_pics = off; off = align_up(off + sizeof(DevPic) * n_pics, 256);
     // error word (+ the row kernel's per-CU workgroup slots, kRowCuSlots x 16 B, intra_rows.h)
-    const size_t o_err = off; off = align_up(off + 256 + kRowCuSlots * 16, 256);
+    // cross-group row kernel (a batch whose chains fit xg workgroups each on the CUs): its progress words
+    // follow the CU slots (cleared together per run), its lines get their own range
+    const bool xg_ok = ctx->xg > 0 && ctx->split && 2 * (long long)n_pics * ctx->xg <= ctx->num_cus;
+    const size_t xg_prog_bytes = xg_ok ? sizeof(int) * 2 * (size_t)g.hc * n_pics : 0;
+    const size_t o_err = off; off = align_up(off + 256 + kRowCuSlots * 16 + xg_prog_bytes, 256);
+    const size_t o_xgl = off;
+    if (xg_ok) off = align_up(off + 2 * (size_t)g.hc * ((size_t)(g.wc + 2) << g.ctb_log2) * n_pics, 256);
     const size_t o_ctus = off; off = align_up(off + sizeof(p265r_ctu) * nc * (size_t)n_pics, 256);
     const size_t o_tbs = off; off = align_up(off + sizeof(p265r_tb) * n_tbs_total, 256);
     // both pools padded by 64 B: the intra kernel reads fixed-shape 32-B runs
@@ -693,7 +711,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     for (int c = 0; c < RC_NUM; ++c) { o_jobs[c] = off; off = align_up(off + sizeof(ResJob) * n_jobs[c], 256); }
     // intra jobs (same index space as the TB records) + per-CTU job counts
     const size_t o_ijobs = off; off = align_up(off + sizeof(IntraJob) * n_tbs_total, 256);
-    const size_t o_jcount = off; off = align_up(off + sizeof(uint32_t) * nc * (size_t)n_pics, 256);
+    const size_t o_jcount = off; off = align_up(off + 2 * sizeof(uint32_t) * nc * (size_t)n_pics, 256);
     size_t o_nf = off;
     size_t nf_bytes = (size_t)g.nf_w * ((g.h + 7) / 8);
     size_t n_nf = 0;
@@ -764,6 +782,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->d_pool = reinterpret_cast<int16_t*>(dbase + o_pool);
     b->d_res = reinterpret_cast<int16_t*>(dbase + o_res);
     b->d_err = reinterpret_cast<int*>(dbase + o_err);
+    b->d_xg_prog = xg_ok ? b->d_err + 64 + kRowCuSlots * 4 : nullptr;
+    b->d_xg_lines = xg_ok ? dbase + o_xgl : nullptr;
     for (int c = 0; c < RC_NUM; ++c) {
         b->d_jobs[c] = reinterpret_cast<ResJob*>(dbase + o_jobs[c]);
         b->n_jobs[c] = n_jobs[c];
@@ -820,7 +840,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         dp.ctus = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus) + (size_t)i * nc;
         dp.tbs = reinterpret_cast<const p265r_tb*>(dbase + o_tbs) + tb_at[i];
         dp.jobs = reinterpret_cast<IntraJob*>(dbase + o_ijobs) + tb_at[i];
-        dp.jcount = reinterpret_cast<uint32_t*>(dbase + o_jcount) + (size_t)i * nc;
+        dp.jcount = reinterpret_cast<uint32_t*>(dbase + o_jcount) + 2 * (size_t)i * nc;
         unsigned char* rec = dbase + o_rec + pic_plane_bytes * i;
         dp.rec[0] = rec;
         dp.rec[1] = rec + align_up(plane_bytes[0], 256);
@@ -1049,7 +1069,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     if (recon && ctx->schedule == 1) {
         // per-CU workgroup slots cleared per run; the error word (d_err[0]) is sticky from upload on,
         // so p265r_batch_status / p265r_batch_download report a give-up in ANY run of the batch
-        HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16, s));
+        // (and the cross-group kernel's progress words behind them)
+        HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16 + (b->d_xg_prog ? sizeof(int) * 2 * (size_t)g.hc * b->n_pics : 0), s));
         // the previous run's loop filters (on the aux stream) read the planes this run writes
         if (b->sao_pending) { HIP_TRY(hipStreamWaitEvent(s, b->sao_done, 0)); b->sao_pending = false; }
         if (ordered && ctx->last_lf_valid) HIP_TRY(hipStreamWaitEvent(s, ctx->last_lf_ev, 0));
@@ -1269,12 +1290,12 @@ int p265r_batch_job_count(p265r_ctx* ctx, p265r_batch* b, uint64_t* luma, uint64
     if (!ctx || !b || !luma || !chroma) return P265R_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    // per CTU slot: luma jobs | chroma jobs << 16 (intra_prep.h), context-size slots per picture
+    // per CTU slot: luma jobs | chroma jobs << 16, top-right indices (intra_prep.h), context-size slots
     const size_t n = (size_t)ctx->n_ctus * b->n_pics;
-    std::vector<uint32_t> jc(n);
-    HIP_TRY(hipMemcpy(jc.data(), b->h_pics[0].jcount, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> jc(2 * n);
+    HIP_TRY(hipMemcpy(jc.data(), b->h_pics[0].jcount, 2 * sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
     uint64_t l = 0, c = 0;
-    for (uint32_t w : jc) { l += w & 0xffffu; c += w >> 16; }
+    for (size_t i = 0; i < n; ++i) { l += jc[2 * i] & 0xffffu; c += jc[2 * i] >> 16; }
     *luma = l;
     *chroma = c;
     return P265R_OK;
@@ -1365,7 +1386,8 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "{\"schedule\": \"%s\", \"row_waves\": %d, \"row_waves_by_run\": \"%s\", \"lean\": %d, "
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
-        "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"phase_order\": %d, "
+        "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"xg\": %d, \"last_launch_xg\": %d, "
+        "\"phase_order\": %d, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : (P265R_PHASE_ORDER
@@ -1373,7 +1395,9 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
                                      "(phase order); small batches (< 1 picture per CU: component split, W=16): side by side; "
                                      "otherwise W=12 while no other lane has a run enqueued since the API synchronised it, "
                                      "else pipe_waves"
-                                   : "small batches (< 1 picture per CU: component split, W=16); otherwise W=12 while no other "
+                                   : "batches of <= CUs / (2 xg) pictures: every luma / chroma chain on xg workgroups of W=4 "
+                                     "(cross-group rows, progress and lines in global memory); small batches (< 1 picture per "
+                                     "CU: component split, W=16); otherwise W=12 while no other "
                                      "lane has a run enqueued since the API synchronised it, else pipe_waves (W=8, 80 VGPRs: "
                                      "the other lanes' residual / prep / SAO waves fit beside it)"),
         ctx->lean, g.fair, g.quad, ctx->luma_lead, ctx->sao_rows, ctx->skip, ctx->debug_sync ? 1 : 0,
@@ -1383,7 +1407,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
 #else
         0,
 #endif
-        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, P265R_PHASE_ORDER,
+        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, ctx->xg, ctx->last_xg ? 1 : 0, P265R_PHASE_ORDER,
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;
     if (size > 0) {
