@@ -76,6 +76,9 @@ struct Geo {                    // batch-uniform geometry
                                 // take that picture's size from pic_geo().  Per-picture arrays keep the
                                 // context-size slots (CTU records, job counts, maps, planes) -- a
                                 // picture's CTU raster and map rows use ITS width in CTUs / 8x8 blocks
+    int tr_check;               // host only: launch the cross-group row kernel's checking instance, which poisons
+                                // the top-right part of a CTU's row-above copy until its wait (checks prep's `tr`
+                                // deterministically; P265R_TR_CHECK, tests)
 };
 
 // ragged-batch support compiled into the kernels (0: A/B only -- a ragged batch then decodes wrongly)

@@ -446,7 +446,12 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
     if (lane == 0) {
         typedef unsigned int u2 __attribute__((ext_vector_type(2)));
         *(__attribute__((address_space(1))) u2*)(P.jcount + 2 * addr) =
-            u2{(uint32_t)n_out | (uint32_t)c_out << 16, (uint32_t)(tr_l < 0 ? n_out : tr_l) | (uint32_t)(tr_c < 0 ? c_out : tr_c) << 16};
+            u2{(uint32_t)n_out | (uint32_t)c_out << 16,
+#ifdef P265R_TR_BROKEN      // negative test of the row kernel's top-right self-check: no job waits
+               (uint32_t)n_out | (uint32_t)c_out << 16};
+#else
+               (uint32_t)(tr_l < 0 ? n_out : tr_l) | (uint32_t)(tr_c < 0 ? c_out : tr_c) << 16};
+#endif
     }
 }
 

@@ -884,7 +884,7 @@ struct XgBuf {
     int xg, seq;                 // workgroups per chain; this run's tag
 };
 
-template <int W, int WPE, bool XG = false>
+template <int W, int WPE, bool XG = false, bool TRCHK = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
 void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
@@ -1129,7 +1129,18 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             const bool early = tr_ctu && tr == 0;               // the first job already reads the top-right CTU
             bool tr_done = !tr_ctu || early;                    // waited for the top-right CTU
             if (cy > 0 && !wait_up(early || !tr_ctu ? min(cx + 2, pwc) : cx + 1)) { failed = true; break; }
-            if (XG && cy > 0) xg_copy(0, (early ? 2 * cts : cts) / 4 + 1);
+            if (XG && cy > 0) {
+                xg_copy(0, (early ? 2 * cts : cts) / 4 + 1);
+                if (TRCHK && !early && tr_ctu) {
+                    // self-check of prep's `tr`: until the top-right wait, its part of the copy holds a
+                    // position-dependent pattern instead of the previous CTU's stale row, so a job before `tr`
+                    // that read it would break parity deterministically rather than by timing
+                    const int h = comp ? lane >> 5 : 0, k = cts / 4 + 1 + (comp ? lane & 31 : lane);
+                    if (k < 2 * cts / 4 + 1)
+                        *reinterpret_cast<uint32_t*>(comp ? &L.ctop[h][4 * k] : &L.ytop[4 * k]) = 0xa55a3cc3u ^ (uint32_t)(k * 0x01030507);
+                    wave_sync();
+                }
+            }
             P265R_TRACE(4 | (cx << 8) | (r << 16));
             const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
             // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr); XG: the wave's copy

@@ -362,7 +362,7 @@ int join_sao(p265r_batch* b) {
     return P265R_OK;
 }
 
-template <int W, int WPE, bool XG = false>
+template <int W, int WPE, bool XG = false, bool TRCHK = false>
 int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     Geo g = ctx->geo;
     // picture slots: the W rows in flight are consecutive in the queue, so they span at
@@ -374,7 +374,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
                kAngTabBytes;
     };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
-    auto fn = intra_rows_kernel<W, WPE, XG>;
+    auto fn = intra_rows_kernel<W, WPE, XG, TRCHK>;
     bool split = false;
     {
         // every workgroup resident at once and holding a single picture: one slot is enough
@@ -450,7 +450,8 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     // after the 12th wait for a whole row to finish)
     // smaller still (every chain on xg CUs of its own): the cross-group kernel, one wave per SIMD
     if (ctx->row_waves == 0 && b->d_xg_prog && 2 * (long long)b->n_pics * ctx->xg <= ctx->num_cus)
-        return launch_rows_w<4, 1, true>(ctx, b, st, alone);
+        return ctx->geo.tr_check ? launch_rows_w<4, 1, true, true>(ctx, b, st, alone)     // (test build of it)
+                                 : launch_rows_w<4, 1, true>(ctx, b, st, alone);
     if (ctx->row_waves == 0 && ctx->split && P265R_SPLIT_W16 && 2 * (long long)b->n_pics <= ctx->num_cus)
         return launch_rows_w<16, 4>(ctx, b, st, alone);
     const int w = ctx->row_waves ? ctx->row_waves : (alone ? 12 : 8);
@@ -517,16 +518,18 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.fair = 1;
     if (const char* v = std::getenv("P265R_FAIR")) g.fair = v[0] != '0';
     g.quad = 3;
+    g.tr_check = 0;
     if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 7;
     ctx->n_ctus = g.wc * g.hc;
     // test knobs of the GPU parity matrix (bench.py refuses to run with any P265R_* variable set)
     for (const char* k : {"P265R_FAIR", "P265R_QUAD", "P265R_SCHEDULE", "P265R_SAO_ROWS", "P265R_LUMA_LEAD", "P265R_ROW_WAVES",
-                          "P265R_FORK_PREP", "P265R_SPLIT", "P265R_XG"})
+                          "P265R_FORK_PREP", "P265R_SPLIT", "P265R_XG", "P265R_TR_CHECK"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';
+    if (const char* v = std::getenv("P265R_TR_CHECK")) g.tr_check = v[0] == '1';
     if (const char* v = std::getenv("P265R_XG")) { const int x = std::atoi(v); ctx->xg = (x == 2 || x == 4 || x == 8) ? x : 0; }
     if (const char* v = std::getenv("P265R_FORK_PREP")) ctx->fork_prep = std::atoi(v) != 0 ? 1 : 0;
     if (const char* v = std::getenv("P265R_ROW_WAVES")) {

@@ -203,7 +203,12 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
         int col[N], e[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) col[k] = t[k * S + lane];
+#ifdef P265R_RES_NOMATH   // timing experiment only (wrong results): the transform's arithmetic removed
+#pragma unroll
+        for (int k = 0; k < N; ++k) e[k] = col[k] << 7;
+#else
         inv_dct_eo<N>(col, e);
+#endif
 #pragma unroll
         for (int y = 0; y < N; ++y) t[y * S + lane] = (int16_t)clamp16i((e[y] + 64) >> 7);
     }
@@ -212,9 +217,22 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
         int row[N], xr[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) row[k] = t[lane * S + k];
+#ifdef P265R_RES_NOMATH
+#pragma unroll
+        for (int k = 0; k < N; ++k) xr[k] = row[k];
+#else
         inv_dct_eo<N>(row, xr);
+#endif
         const int bd2 = 20 - bit_depth;
         const int rnd2 = 1 << (bd2 - 1);
+#ifdef P265R_RES_PADV     // timing experiment only: P265R_RES_PADV dependent VALU per thread
+        {
+            uint32_t z = (uint32_t)lane;
+#pragma unroll
+            for (int q = 0; q < P265R_RES_PADV; ++q) asm volatile("v_add_u32 %0, 1, %0" : "+v"(z));
+            asm volatile("" :: "v"(z));
+        }
+#endif
 #pragma unroll
         for (int v = 0; v < N / 8; ++v) {
             uint32_t o[4];

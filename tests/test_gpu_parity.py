@@ -48,11 +48,14 @@ def _check(recon_mod, params, pics, label=""):
 # and leading by more rows than a picture has (40); small batches run their luma and chroma chains on
 # two workgroups per picture unless P265R_SPLIT=0 (the large-batch layout, which the bench runs), and
 # smaller ones each chain on P265R_XG workgroups of 4 waves with progress and lines in global memory
-# (default 4, "rows_auto"; 2 and 8; 0: the one-workgroup-per-chain W = 16 layout).  (W = 4 / 6 / 10 / 16
+# (default 4, "rows_auto"; 2 and 8; 0: the one-workgroup-per-chain W = 16 layout); P265R_TR_CHECK=1 poisons
+# the top-right part of a CTU's row-above copy until the top-right wait, so a job the prep kernel placed
+# before that wait but which reads the top-right CTU fails parity deterministically (not by timing).  (W = 4 / 6 / 10 / 16
 # and the unconstrained W = 8 build exist only in the experiments build, p265r.hip P265R_EXPERIMENTS.)
 ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
                 "rows_nosplit": {"P265R_SPLIT": "0"},
-                "rows_w16": {"P265R_XG": "0"}, "rows_xg2": {"P265R_XG": "2"}, "rows_xg8": {"P265R_XG": "8"},
+                "rows_w16": {"P265R_XG": "0"}, "rows_xg2": {"P265R_XG": "2", "P265R_TR_CHECK": "1"},
+                "rows_xg8": {"P265R_XG": "8", "P265R_TR_CHECK": "1"}, "rows_xgchk": {"P265R_TR_CHECK": "1"},
                 "rows_nofair": {"P265R_ROW_WAVES": "12", "P265R_FAIR": "0", "P265R_FORK_PREP": "0", "P265R_SPLIT": "0"},
                 "rows_lead0": {"P265R_ROW_WAVES": "8", "P265R_LUMA_LEAD": "0", "P265R_SPLIT": "0"},
                 "rows12": {"P265R_ROW_WAVES": "12"},
@@ -63,7 +66,7 @@ ROW_VARIANTS = {"rows": {"P265R_ROW_WAVES": "8"}, "rows_auto": {},
                 "rows_saostrip": {"P265R_ROW_WAVES": "8", "P265R_SAO_ROWS": "2"}}
 
 
-@pytest.fixture(params=["rows", "rows_auto", "rows_nosplit", "rows_w16", "rows_xg2", "rows_xg8", "steps", "rows_nofair", "rows_lead0", "rows12", "rows_lead40", "rows_quad1",
+@pytest.fixture(params=["rows", "rows_auto", "rows_nosplit", "rows_w16", "rows_xg2", "rows_xg8", "rows_xgchk", "steps", "rows_nofair", "rows_lead0", "rows12", "rows_lead40", "rows_quad1",
                         "rows_noquad", "rows_lf", "rows_saostrip"])
 def schedule(request, monkeypatch):
     """Both intra schedules (CU-local row pipeline, W = 8 and 12, with and without the luma / chroma
