@@ -170,6 +170,9 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
         };
     };
 };
+#ifndef P265R_LATE_REC
+#define P265R_LATE_REC 0                 // 1: the next job's record read after the job (A/B: slower)
+#endif
 #ifndef P265R_TR_SEG
 #define P265R_TR_SEG 0                   // 1: the job loop in two segments around the top-right wait
 #endif
@@ -1217,9 +1220,6 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 rn = issue(cur, 0);
             }
             pre = false;
-#ifdef P265R_JOB_UNROLL
-#pragma unroll P265R_JOB_UNROLL
-#endif
             // the top-right wait before job tr (the row above the CTU suffices for the jobs before it)
 #if P265R_TR_SEG
             // two segments: jobs [0, tr), the top-right wait, jobs [tr, nt) (no per-job test)
@@ -1235,6 +1235,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             for (; t < t_end; ++t) {
 #else
             const int t_trw = tr_done || tr >= nt ? -1 : tr;
+#ifdef P265R_JOB_UNROLL
+#pragma unroll P265R_JOB_UNROLL
+#endif
             for (int t = 0; t < nt; ++t) {
                 if (t == t_trw) {                       // (a failed wait runs on; the loop exits after the job)
                     failed = !wait_up(cx + 2);
@@ -1251,8 +1254,16 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int c16 = (int)rn.x, c16m = (int)rn.y;
                 if (t + 1 < nt) {
                     if (((t + 1) & 63) == 0) refill(t + 1);
+#if P265R_LATE_REC
+                    // the next record's residual fields only (its whole record is read after this job, into
+                    // the registers this one held: no per-job copies of the six record words)
+                    const int l = (t + 1) & 63;
+                    auto rl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane(v, l); };
+                    rn = issue(JobS{rl(rec0.x), 0u, 0u, rl(rec0.w), rl(rec1.x), rl(rec1.y)}, t + 1);
+#else
                     cur = sjob(t + 1);
                     rn = issue(cur, t + 1);
+#endif
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
 #ifdef P265R_PAD_SALU
@@ -1325,6 +1336,9 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                         __hip_atomic_fetch_add(&ctl.pad[2 * jc + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
+#endif
+#if P265R_LATE_REC
+                if (t + 1 < nt) cur = sjob(t + 1);
 #endif
             }
 #if P265R_TR_SEG
