@@ -170,6 +170,12 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
         };
     };
 };
+// timing experiment (wrong output): every residual load of the row kernel inside one 8-KB window
+#ifdef P265R_RES_FAKE
+#define P265R_RI(x) ((x) & 4095)
+#else
+#define P265R_RI(x) (x)
+#endif
 #ifndef P265R_LATE_REC
 #define P265R_LATE_REC 0                 // 1: the next job's record read after the job (A/B: slower)
 #endif
@@ -1162,13 +1168,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int ls = 2 * lg - (pr ? 5 : 6);
                 const int S = ls > 0 ? (1 << ls) : 1;
                 const int sidx = hl * S < (1 << (2 * lg)) ? hl * S : 0;
-                return reinterpret_cast<const uint4*>(resid + (int)(h ? w4 : w3) + (sidx & ~7));
+                return reinterpret_cast<const uint4*>(resid + P265R_RI((int)(h ? w4 : w3)) + (sidx & ~7));
             };
             // fast jobs (J5_FAST): one residual sample per lane (2-B load); w3 / w4 already point
             // at the pool, the residual or the zero block, and lanes past the TB read padding
             auto res_fast = [&](uint32_t w0, uint32_t w3, uint32_t w4) {
                 const bool pr = (w0 >> 15) & 3u;
-                return resid + (int)(pr && lane >= 32 ? w4 : w3) + (pr ? (lane & 31) : lane);
+                return resid + P265R_RI((int)(pr && lane >= 32 ? w4 : w3)) + (pr ? (lane & 31) : lane);
             };
             // job records (24 B): 64 at a time into six VGPRs per lane, read per job with v_readlane
             // (scalar loads were measured slower: their lgkmcnt waits serialise with the LDS
@@ -1193,7 +1199,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 if (j.w5 & J5_QUAD) {                       // quads: residual = w3 + 16 * code (15: the zero block)
                     const int q = ((lane >> 4) & 2) | ((lane >> 2) & 1);    // sub-TB of sample (x, y) of the 8x8 region
                     const int i = ((lane >> 1) & 12) + (lane & 3);          // sample index in the 4x4 sub-TB
-                    auto at = [&](uint32_t code) { return (code == 15u ? zero_res : (int)j.w3 + (int)(code << 4)) + i; };
+                    auto at = [&](uint32_t code) { return P265R_RI(code == 15u ? zero_res : (int)j.w3 + (int)(code << 4)) + i; };
                     if ((j.w0 >> 15) & 3u) {                                // chroma: Cb | Cr << 16, codes at 8q + 4h
                         const uint32_t codes = j.w4 >> (8 * q);
                         const uint32_t cb = (uint16_t)*gptr(resid + at(codes & 15u));
@@ -1202,11 +1208,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                     }
                     return u32x2_t{(uint32_t)(int)*gptr(resid + at((j.w4 >> (4 * q)) & 15u)), 0u};
                 } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 15u) == 13u) { // Cb+Cr 8x8: Cb | Cr << 16 of sample lane
-                    const uint32_t cb = (uint16_t)*gptr(resid + (int)j.w3 + lane);
-                    const uint32_t cr = (uint16_t)*gptr(resid + (int)j.w4 + lane);
+                    const uint32_t cb = (uint16_t)*gptr(resid + P265R_RI((int)j.w3) + lane);
+                    const uint32_t cr = (uint16_t)*gptr(resid + P265R_RI((int)j.w4) + lane);
                     return u32x2_t{cb, cr};     // packed at use: no wait here
                 } else if ((j.w5 & J5_FAST) && ((j.w0 >> 13) & 3u) == 2u) { // 16x16 luma: 4 samples per lane
-                    const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(resid + (int)j.w3 + 4 * lane));
+                    const u32x2_t d = *reinterpret_cast<const P265R_GLOBAL u32x2_t*>(gptr(resid + P265R_RI((int)j.w3) + 4 * lane));
                     return d;
                 } else if (j.w5 & J5_FAST) {
                     return u32x2_t{(uint32_t)(int)*gptr(res_fast(j.w0, j.w3, j.w4)), 0u};
