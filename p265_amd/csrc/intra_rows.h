@@ -179,9 +179,6 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
 #ifndef P265R_LATE_REC
 #define P265R_LATE_REC 0                 // 1: the next job's record read after the job (A/B: slower)
 #endif
-#ifndef P265R_TR_SEG
-#define P265R_TR_SEG 0                   // 1: the job loop in two segments around the top-right wait
-#endif
 #ifndef P265R_TR_DEFER
 #define P265R_TR_DEFER 1                 // 0: wait for the top-right CTU before the CTU starts (A/B knob)
 #endif
@@ -1067,11 +1064,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         // CTU header (first TB index | job counts) loaded one CTU ahead, and the next CTU's first
         // 64 job records loaded right after this CTU's last job: a CTU then starts with its
         // records in registers (one dependent round trip, its first residual, instead of three)
-        // (jcount: two words per CTU -- the job counts and the index of each list's first job that
-        // reads the top-right CTU, intra_prep.h)
+        // (jcount: four words per CTU -- the job counts, each list's first job that reads the top-right
+        // CTU, each list's first job in the bottom-right quadrant, intra_prep.h)
         auto hdr_load = [&](int a) {
-            const uint2 jp = gload(reinterpret_cast<const uint2*>(jcount + 2 * a));
-            return make_uint4(gload(reinterpret_cast<const uint2*>(ctus + a)).x, jp.x, jp.y, 0u);
+            const uint4 jp = gload(reinterpret_cast<const uint4*>(jcount + 4 * a));
+            return make_uint4(gload(reinterpret_cast<const uint2*>(ctus + a)).x, jp.x, jp.y, jp.z);
         };
         uint4 hdr_n = hdr_load(cy * pwc);
 #ifndef P265R_ROW_PRIO
@@ -1105,6 +1102,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             const uint32_t tb_begin = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
             const uint32_t jc = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
             const uint32_t trw = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.z);
+            const uint32_t brw = XG ? (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.w) : 0u;
             if (cx + 1 < pwc) hdr_n = hdr_load(addr + 1);    // in flight during this CTU
             const int n_chroma = (int)(jc >> 16);
             const int nt = comp ? n_chroma : (int)(jc & 0xffffu);
@@ -1113,6 +1111,13 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             constexpr bool kDefer = P265R_TR_DEFER && (XG || W == 16);
             const int tr = !kDefer ? 0 : comp ? (int)(trw >> 16) : (int)(trw & 0xffffu);   // first job reading the top-right CTU
             const bool tr_ctu = cy > 0 && cx + 1 < pwc;        // a top-right CTU exists (else nothing to wait for)
+            // XG progress counts half CTUs (2 per finished CTU, +1 once the left half of the next one's bottom
+            // row is out): at CTB 64 a TB reaches at most half a CTB into the top-right CTU (TBs <= 32 luma,
+            // 16 chroma), whose left bottom half is final after its bottom-left quadrant (prep: `br`)
+            const bool halfp = XG && g.ctb_log2 == 6;
+            const int u = XG ? 2 : 1;                          // progress units per CTU
+            const int need_tr = halfp ? 2 * (cx + 1) + 1 : u * min(cx + 2, pwc);
+            const int br = XG ? (comp ? (int)(brw >> 16) : (int)(brw & 0xffffu)) : 0;
             auto up_ready = [&](int need) {
                 const int v = XG ? __hip_atomic_load(xg_prog + (cy - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                  : __hip_atomic_load(up_prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1135,20 +1140,37 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 wave_sync();
             };
             auto wait_up = [&](int need) { return wait_until([&] { return up_ready(need); }); };
+            // XG: the bottom row's first nd dwords of this chain's plane(s) into line cy, completed, then the
+            // progress word 2 cx + half (half = 1: the left half, mid-CTU; the CTU's end writes the whole row)
+            auto xg_publish = [&](int nd, int half) {
+                const int h = comp ? lane >> 5 : 0, k = comp ? lane & 31 : lane;
+                const int hv = min(cts, (comp ? ph >> 1 : ph) - (y0 >> comp));
+                if (k < nd) {
+                    const uint8_t* src = (comp ? L.c[h] : L.y) + (hv - 1) * (comp ? 32 : 64) + 4 * k;
+                    P265R_GLOBAL uint8_t* dl = xg_line + (size_t)cy * xg_row_bytes + (size_t)h * (xg_row_bytes >> 1) +
+                                               cts + (x0 >> comp) + 4 * k;
+                    __hip_atomic_store(reinterpret_cast<P265R_GLOBAL uint32_t*>(dl), *reinterpret_cast<const uint32_t*>(src),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(xg_prog + cy, tag | (2 * cx + half), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
             const bool early = tr_ctu && tr == 0;               // the first job already reads the top-right CTU
             bool tr_done = !tr_ctu || early;                    // waited for the top-right CTU
-            if (cy > 0 && !wait_up(early || !tr_ctu ? min(cx + 2, pwc) : cx + 1)) { failed = true; break; }
+            if (cy > 0 && !wait_up(early ? need_tr : u * (cx + 1))) { failed = true; break; }
+            // (XG) the top-right part of the row above: its left half at CTB 64, all of it otherwise
+            const int tr_k1 = (halfp ? cts + cts / 2 : 2 * cts) / 4 + 1;
             if (XG && cy > 0) {
-                xg_copy(0, (early ? 2 * cts : cts) / 4 + 1);
-                if (TRCHK && !early && tr_ctu) {
-                    // self-check of prep's `tr`: until the top-right wait, its part of the copy holds a
-                    // position-dependent pattern instead of the previous CTU's stale row, so a job before `tr`
-                    // that read it would break parity deterministically rather than by timing
+                if (TRCHK && tr_ctu) {
+                    // self-check of prep's `tr` (and of the half-CTB reach): the whole top-right part of the copy
+                    // holds a position-dependent pattern until its wait (the right half at CTB 64 for good),
+                    // so a job that read it early would break parity deterministically rather than by timing
                     const int h = comp ? lane >> 5 : 0, k = cts / 4 + 1 + (comp ? lane & 31 : lane);
                     if (k < 2 * cts / 4 + 1)
                         *reinterpret_cast<uint32_t*>(comp ? &L.ctop[h][4 * k] : &L.ytop[4 * k]) = 0xa55a3cc3u ^ (uint32_t)(k * 0x01030507);
                     wave_sync();
                 }
+                xg_copy(0, early ? tr_k1 : cts / 4 + 1);
             }
             P265R_TRACE(4 | (cx << 8) | (r << 16));
             const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
@@ -1227,30 +1249,18 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             }
             pre = false;
             // the top-right wait before job tr (the row above the CTU suffices for the jobs before it)
-#if P265R_TR_SEG
-            // two segments: jobs [0, tr), the top-right wait, jobs [tr, nt) (no per-job test)
-            int t = 0;
-#pragma unroll 1
-            for (int seg = tr_done || tr >= nt ? 1 : 0; seg < 2; ++seg) {
-            if (seg == 1 && !tr_done) {
-                if (!wait_up(cx + 2)) { failed = true; break; }
-                if (XG) xg_copy(cts / 4 + 1, 2 * cts / 4 + 1);
-                tr_done = true;
-            }
-            const int t_end = seg == 0 ? tr : nt;
-            for (; t < t_end; ++t) {
-#else
             const int t_trw = tr_done || tr >= nt ? -1 : tr;
+            const int t_half = halfp && br < nt ? br : -1;     // XG: publish the bottom row's left half first
 #ifdef P265R_JOB_UNROLL
 #pragma unroll P265R_JOB_UNROLL
 #endif
             for (int t = 0; t < nt; ++t) {
                 if (t == t_trw) {                       // (a failed wait runs on; the loop exits after the job)
-                    failed = !wait_up(cx + 2);
-                    if (XG) xg_copy(cts / 4 + 1, 2 * cts / 4 + 1);
+                    failed = !wait_up(need_tr);
+                    if (XG) xg_copy(cts / 4 + 1, tr_k1);
                     tr_done = true;
                 }
-#endif
+                if (XG && t == t_half) xg_publish(cts / 8, 1);
 #ifdef P265R_JOB_STATS
                 const long long tj0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1347,9 +1357,6 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 if (t + 1 < nt) cur = sjob(t + 1);
 #endif
             }
-#if P265R_TR_SEG
-            }
-#endif
             if (failed) break;                             // (wait_until published the error)
             // before this CTU's bottom row goes into the line buffer (whether or not a job read it; XG:
             // one line per row, nothing to overwrite)
@@ -1419,7 +1426,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 // the line's stores complete (at the agent's coherence point) before the progress word
                 // that announces them; the plane stores are read only by later kernels
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_store(xg_prog + cy, tag | (cx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) __hip_atomic_store(xg_prog + cy, tag | (2 * (cx + 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }

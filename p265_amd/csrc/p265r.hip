@@ -714,7 +714,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     for (int c = 0; c < RC_NUM; ++c) { o_jobs[c] = off; off = align_up(off + sizeof(ResJob) * n_jobs[c], 256); }
     // intra jobs (same index space as the TB records) + per-CTU job counts
     const size_t o_ijobs = off; off = align_up(off + sizeof(IntraJob) * n_tbs_total, 256);
-    const size_t o_jcount = off; off = align_up(off + 2 * sizeof(uint32_t) * nc * (size_t)n_pics, 256);
+    const size_t o_jcount = off; off = align_up(off + 4 * sizeof(uint32_t) * nc * (size_t)n_pics, 256);
     size_t o_nf = off;
     size_t nf_bytes = (size_t)g.nf_w * ((g.h + 7) / 8);
     size_t n_nf = 0;
@@ -843,7 +843,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         dp.ctus = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus) + (size_t)i * nc;
         dp.tbs = reinterpret_cast<const p265r_tb*>(dbase + o_tbs) + tb_at[i];
         dp.jobs = reinterpret_cast<IntraJob*>(dbase + o_ijobs) + tb_at[i];
-        dp.jcount = reinterpret_cast<uint32_t*>(dbase + o_jcount) + 2 * (size_t)i * nc;
+        dp.jcount = reinterpret_cast<uint32_t*>(dbase + o_jcount) + 4 * (size_t)i * nc;
         unsigned char* rec = dbase + o_rec + pic_plane_bytes * i;
         dp.rec[0] = rec;
         dp.rec[1] = rec + align_up(plane_bytes[0], 256);
@@ -1295,10 +1295,10 @@ int p265r_batch_job_count(p265r_ctx* ctx, p265r_batch* b, uint64_t* luma, uint64
     HIP_TRY(hipStreamSynchronize(b->stream));
     // per CTU slot: luma jobs | chroma jobs << 16, top-right indices (intra_prep.h), context-size slots
     const size_t n = (size_t)ctx->n_ctus * b->n_pics;
-    std::vector<uint32_t> jc(2 * n);
-    HIP_TRY(hipMemcpy(jc.data(), b->h_pics[0].jcount, 2 * sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> jc(4 * n);
+    HIP_TRY(hipMemcpy(jc.data(), b->h_pics[0].jcount, 4 * sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
     uint64_t l = 0, c = 0;
-    for (size_t i = 0; i < n; ++i) { l += jc[2 * i] & 0xffffu; c += jc[2 * i] >> 16; }
+    for (size_t i = 0; i < n; ++i) { l += jc[4 * i] & 0xffffu; c += jc[4 * i] >> 16; }
     *luma = l;
     *chroma = c;
     return P265R_OK;
