@@ -429,6 +429,9 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
 // alone: no other lane of the context has a run enqueued (ctx->lane_busy), so this batch's kernels
 // have the GPU to themselves: W = 12 with fair CU sharing; otherwise W = 8 (80 VGPRs, so the residual /
 // prep / SAO waves of the neighbouring batches fit beside it on every SIMD)
+#ifndef P265R_W10_WPE
+#define P265R_W10_WPE 5                  // experiments: the pipelined W = 10 build's waves-per-SIMD attribute
+#endif
 int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
 #if P265R_EXPERIMENTS
     switch (ctx->row_waves) {
@@ -441,7 +444,7 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 4) return launch_rows_w<4, 1>(ctx, b, st, alone);
     if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 6) return launch_rows_w<6, 1>(ctx, b, st, alone);
     if (ctx->row_waves == 0 && !alone && ctx->pipe_waves == 10 && !(ctx->split && 2 * (long long)b->n_pics <= ctx->num_cus))
-        return launch_rows_w<10, 5>(ctx, b, st, alone);
+        return launch_rows_w<10, P265R_W10_WPE>(ctx, b, st, alone);
     if (ctx->lean == 0 && (ctx->row_waves == 8 || (ctx->row_waves == 0 && !alone))) return launch_rows_w<8, 1>(ctx, b, st, alone);
 #endif
     // a batch small enough for the component split with one workgroup per CU (the latency regime:
