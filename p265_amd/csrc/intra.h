@@ -82,6 +82,16 @@ struct Geo {                    // batch-uniform geometry
                                 // deterministically; P265R_TR_CHECK, tests)
 };
 
+// A/B: s_setprio of the bandwidth-phase kernels' waves (residual, prep, SAO), 0 = default
+#ifndef P265R_BW_PRIO
+#define P265R_BW_PRIO 0
+#endif
+#if P265R_BW_PRIO > 0
+#define P265R_BW_PRIO_SET() __builtin_amdgcn_s_setprio(P265R_BW_PRIO)
+#else
+#define P265R_BW_PRIO_SET() do { } while (0)
+#endif
+
 // ragged-batch support compiled into the kernels (0: A/B only -- a ragged batch then decodes wrongly)
 #ifndef P265R_RAGGED
 #define P265R_RAGGED 1

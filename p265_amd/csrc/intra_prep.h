@@ -218,6 +218,7 @@ __device__ __forceinline__ uint32_t job_w1(uint32_t w0, uint32_t w5, uint32_t an
 __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict__ pics, Geo g, BatchView v) {
     __shared__ LumaJobLds sj[kMaxCtuLuma];
     __shared__ ChromaJobLds sc[kMaxCtuChroma];
+    P265R_BW_PRIO_SET();
     const DevPic P = pics[blockIdx.z];
     // CTU records from the batch layout (no wait for the DevPic load: both in flight together;
     // slots of the context size, a ragged batch's smaller pictures use the front of theirs)

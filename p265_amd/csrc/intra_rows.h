@@ -176,6 +176,9 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
 #else
 #define P265R_RI(x) (x)
 #endif
+#ifndef P265R_PIPE_PRIO
+#define P265R_PIPE_PRIO 0                // A/B: s_setprio of the pipelined (W = 8) row kernel's waves
+#endif
 #ifndef P265R_LATE_REC
 #define P265R_LATE_REC 0                 // 1: the next job's record read after the job (A/B: slower)
 #endif
@@ -941,6 +944,10 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     if (P265R_ANGTAB8)
         for (int i = threadIdx.x; i < 35 * 64; i += 64 * W) atab[35 * 16 + i] = angtab_entry<3>(i >> 6, i & 63);
     __syncthreads();
+#if P265R_PIPE_PRIO > 0
+    // A/B: the pipelined build's waves issue ahead of the other lanes' residual / prep / SAO waves
+    if (W == 8 && !split) __builtin_amdgcn_s_setprio(P265R_PIPE_PRIO);
+#endif
 
     const int G = split ? (int)(gridDim.x >> 1) : (int)gridDim.x;
     const int b = split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;

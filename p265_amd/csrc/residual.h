@@ -86,6 +86,7 @@ __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restric
                                                         int16_t* __restrict__ res,
                                                         const ResJob* __restrict__ jobs, int n_jobs,
                                                         int bit_depth, uint32_t slab) {
+    P265R_BW_PRIO_SET();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_jobs) return;
     const ResJob jb = jobs[i];
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
                                                        int16_t* __restrict__ res,
                                                        const ResJob* __restrict__ jobs, int n_jobs,
                                                        int bit_depth_luma, int bit_depth_chroma, uint32_t slab) {
+    P265R_BW_PRIO_SET();
     constexpr int N = 1 << LOG2;
     constexpr int TPB = 256 / N;                 // TBs per block
     constexpr int S = N + 2;                     // padded LDS row (odd dword stride)

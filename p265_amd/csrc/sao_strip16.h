@@ -76,6 +76,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
         const DevPic* __restrict__ pics, Geo g, BatchView v, int n_pics) {
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) uint8_t gu8;
+    P265R_BW_PRIO_SET();
     const int lane = threadIdx.x & 63;
     const int per_pic = sao16_units(g);
     const int total = per_pic * n_pics;
