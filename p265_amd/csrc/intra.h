@@ -39,7 +39,7 @@ struct DevPic {                 // per picture, device-resident table
     IntraJob* jobs;             // same index space as tbs (jobs of a CTU start at tb_begin)
     uint32_t* jcount;           // per CTU four words: luma jobs | chroma jobs << 16 (chroma listed first), the
                                 // index of the first job of each list that reads the top-right CTU, the index of
-                                // the first job in the CTB's bottom-right quadrant, 0 (intra_prep.h)
+                                // one past the last job in the CTB's bottom-left quadrant, 0 (intra_prep.h)
     uint8_t* dbk_map;           // per 8x8 luma block (loopfilter.h), nullptr without deblocking
     int32_t  pool_rel;          // residual pool element index of coefficient pool element 0 (<= 0)
     uint32_t zero_off;          // residual pool element index of a 256-sample zero block

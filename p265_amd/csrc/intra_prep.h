@@ -394,18 +394,22 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const int reach = quad ? xr + 12 : xr + (8 << ((w0 >> 13) & 3u));
         return (yr == 0) & (reach > (chroma ? ctb >> 1 : ctb)) & ((flags & 8u) != 0u);
     };
-    // does a job lie in the CTB's bottom-right quadrant?  Every job before the first such one completes the
-    // left half of the CTB's bottom row (z-order: the bottom-left quadrant precedes it), which the row below
-    // may then read as its top-right samples (intra_rows.h, cross-group kernel at CTB 64)
-    auto in_br = [&](uint32_t w0, bool chroma) -> bool {
+    // does a job lie in the CTB's bottom-left quadrant?  Once the last such job of the list (either chroma
+    // plane: a component-major TB order lists every Cb job before the Cr ones) has run, the left half of the
+    // CTB's bottom row is final -- no other job writes it (TBs never straddle a quadrant at CTB 64) -- and the
+    // row below may read it as its top-right samples (intra_rows.h, cross-group kernel at CTB 64)
+    auto in_bl = [&](uint32_t w0, bool chroma) -> bool {
         const uint32_t o = (w0 & 0x1fffu) - (chroma ? 4096u : 0u);
         const int hq = chroma ? ctb >> 2 : ctb >> 1;
-        return ((int)(o & (chroma ? 31u : 63u)) >= hq) & ((int)(o >> (chroma ? 5 : 6)) >= hq);
+        return ((int)(o & (chroma ? 31u : 63u)) < hq) & ((int)(o >> (chroma ? 5 : 6)) >= hq);
+    };
+    auto last_of = [&](unsigned long long m, unsigned long long me, int out) {    // index of m's last job
+        return m ? out + (int)__popcll(me & ((2ull << (63 - __clzll((long long)m))) - 1ull)) - 1 : -1;
     };
     auto first_of = [&](unsigned long long m, unsigned long long me, int out) {   // index of m's first job
         return m ? out + (int)__popcll(me & ((1ull << (__ffsll((long long)m) - 1)) - 1ull)) : -1;
     };
-    int c_out = 0, tr_c = -1, br_c = -1;
+    int c_out = 0, tr_c = -1, bl_c = -1;
     unsigned long long hp = 0;
     for (int base = 0; base < n_chroma; base += 64) {
         const int s = base + lane;
@@ -429,10 +433,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         }
         if (emit) prep_job_store(jobs + c_out + rank(me_), J);
         if (tr_c < 0) tr_c = first_of(__ballot(emit && needs_tr(J.w[0], hd, true)), me_, c_out);
-        if (br_c < 0) br_c = first_of(__ballot(emit && in_br(J.w[0], true)), me_, c_out);
+        bl_c = max(bl_c, last_of(__ballot(emit && in_bl(J.w[0], true)), me_, c_out));
         c_out += __popcll(me_);
     }
-    int n_out = 0, tr_l = -1, br_l = -1;
+    int n_out = 0, tr_l = -1, bl_l = -1;
     hp = 0;
     for (int base = 0; base < n_luma; base += 64) {
         const int s = base + lane;
@@ -449,11 +453,12 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const IntraJob J = hd ? make_quad(sj + sq, qb, qc) : luma_job(l, P.zero_off, w1);
         if (emit) prep_job_store(jobs + c_out + n_out + rank(me_), J);
         if (tr_l < 0) tr_l = first_of(__ballot(emit && needs_tr(J.w[0], hd, false)), me_, n_out);
-        if (br_l < 0) br_l = first_of(__ballot(emit && in_br(J.w[0], false)), me_, n_out);
+        bl_l = max(bl_l, last_of(__ballot(emit && in_bl(J.w[0], false)), me_, n_out));
         n_out += __popcll(me_);
     }
     // per CTU, luma | chroma << 16 each: job counts; the index of the first job that reads the top-right
-    // CTU; the index of the first job in the bottom-right quadrant (both = the count when there is none)
+    // CTU (= the count when none does); one past the last job in the bottom-left quadrant (= the count when
+    // there is none: a CTU row below the picture's last sample row has no reader)
     if (lane == 0) {
         typedef unsigned int u4 __attribute__((ext_vector_type(4)));
         *(__attribute__((address_space(1))) u4*)(P.jcount + 4 * addr) =
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
 #else
                (uint32_t)(tr_l < 0 ? n_out : tr_l) | (uint32_t)(tr_c < 0 ? c_out : tr_c) << 16,
 #endif
-               (uint32_t)(br_l < 0 ? n_out : br_l) | (uint32_t)(br_c < 0 ? c_out : br_c) << 16, 0u};
+               (uint32_t)(bl_l < 0 ? n_out : bl_l + 1) | (uint32_t)(bl_c < 0 ? c_out : bl_c + 1) << 16, 0u};
     }
 }
 

@@ -176,6 +176,9 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
 #else
 #define P265R_RI(x) (x)
 #endif
+#ifndef P265R_XG_PRE
+#define P265R_XG_PRE 0                   // XG: the next CTU's first residual fetched at the publish (A/B knob)
+#endif
 #ifndef P265R_PIPE_PRIO
 #define P265R_PIPE_PRIO 0                // A/B: s_setprio of the pipelined (W = 8) row kernel's waves
 #endif
@@ -1072,7 +1075,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         // 64 job records loaded right after this CTU's last job: a CTU then starts with its
         // records in registers (one dependent round trip, its first residual, instead of three)
         // (jcount: four words per CTU -- the job counts, each list's first job that reads the top-right
-        // CTU, each list's first job in the bottom-right quadrant, intra_prep.h)
+        // CTU, one past each list's last job in the bottom-left quadrant, intra_prep.h)
         auto hdr_load = [&](int a) {
             const uint4 jp = gload(reinterpret_cast<const uint4*>(jcount + 4 * a));
             return make_uint4(gload(reinterpret_cast<const uint2*>(ctus + a)).x, jp.x, jp.y, jp.z);
@@ -1096,6 +1099,11 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
         uint4 rec0 = make_uint4(0, 0, 0, 0);
         uint2 rec1 = make_uint2(0, 0);
         bool pre = false;                                  // rec0 / rec1 hold this CTU's first records
+        // XG: the next CTU's first job record and residual, fetched after this CTU's publish (its
+        // residual load then overlaps the next CTU's dependency poll and row-above copy)
+        uint32_t pj0 = 0, pj1 = 0, pj2 = 0, pj3 = 0, pj4 = 0, pj5 = 0;
+        u32x2_t rn_pre = {0u, 0u};
+        bool pre_issued = false;
         for (int cx = 0; cx < pwc; ++cx) {
             // ---- wait for the row above -------------------------------------------------
             // The CTU above (1-CTU lag) before the CTU starts; the top-right CTU (2-CTU lag) before the
@@ -1120,7 +1128,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             const bool tr_ctu = cy > 0 && cx + 1 < pwc;        // a top-right CTU exists (else nothing to wait for)
             // XG progress counts half CTUs (2 per finished CTU, +1 once the left half of the next one's bottom
             // row is out): at CTB 64 a TB reaches at most half a CTB into the top-right CTU (TBs <= 32 luma,
-            // 16 chroma), whose left bottom half is final after its bottom-left quadrant (prep: `br`)
+            // 16 chroma), whose left bottom half is final after its bottom-left quadrant's jobs (prep: `br`)
             const bool halfp = XG && g.ctb_log2 == 6;
             const int u = XG ? 2 : 1;                          // progress units per CTU
             const int need_tr = halfp ? 2 * (cx + 1) + 1 : u * min(cx + 2, pwc);
@@ -1250,11 +1258,17 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             };
             JobS cur{0, 0, 0, 0, 0, 0};
             if (nt) {
-                if (!pre) refill(0);
-                cur = sjob(0);
-                rn = issue(cur, 0);
+                if (XG && pre_issued) {
+                    cur = JobS{pj0, pj1, pj2, pj3, pj4, pj5};
+                    rn = rn_pre;
+                } else {
+                    if (!pre) refill(0);
+                    cur = sjob(0);
+                    rn = issue(cur, 0);
+                }
             }
             pre = false;
+            pre_issued = false;
             // the top-right wait before job tr (the row above the CTU suffices for the jobs before it)
             const int t_trw = tr_done || tr >= nt ? -1 : tr;
             const int t_half = halfp && br < nt ? br : -1;     // XG: publish the bottom row's left half first
@@ -1369,11 +1383,12 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             // one line per row, nothing to overwrite)
             if (!XG && !tr_done && !wait_up(cx + 2)) { failed = true; break; }
 
+            int nt2 = 0;
             if (cx + 1 < pwc) {                            // the next CTU's first 64 job records
                 const uint32_t tb2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.x);
                 const uint32_t jc2 = (uint32_t)__builtin_amdgcn_readfirstlane(hdr_n.y);
                 const int nc2 = (int)(jc2 >> 16);
-                const int nt2 = comp ? nc2 : (int)(jc2 & 0xffffu);
+                nt2 = comp ? nc2 : (int)(jc2 & 0xffffu);
                 const IntraJob* jl2 = jobs + tb2 + (comp ? 0 : nc2);
                 if (lane < nt2) { rec0 = ld16(&jl2[lane].w[0]); rec1 = ld8(&jl2[lane].w[4]); }
                 else { rec0 = make_uint4(0, 0, 0, 0); rec1 = make_uint2(0, 0); }
@@ -1434,6 +1449,12 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 // that announces them; the plane stores are read only by later kernels
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store(xg_prog + cy, tag | (2 * (cx + 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (P265R_XG_PRE && pre && nt2 > 0) {     // (the wait above also covered the record loads)
+                    const JobS c0 = sjob(0);
+                    pj0 = c0.w0; pj1 = c0.w1; pj2 = c0.w2; pj3 = c0.w3; pj4 = c0.w4; pj5 = c0.w5;
+                    rn_pre = issue(c0, 0);
+                    pre_issued = true;
+                }
             } else {
                 __hip_atomic_store(my_prog, tag | (cx + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
