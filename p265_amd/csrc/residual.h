@@ -160,6 +160,57 @@ __device__ __forceinline__ void inv_dct_eo(const int (&c)[N], int (&x)[N]) {
     }
 }
 
+// The same butterfly with the odd parts as packed 16-bit dot products: every input of either stage is an
+// int16 (dequantised coefficients and the stage-1 output are clipped to 16 bits), so two odd coefficients
+// pack into one register and one v_dot2c_i32_i16 with a literal pair of matrix entries adds two products
+// into the 32-bit sum (exact: |sum| < 2^15 * 90 * 32 < 2^31).  About half the multiply-add instructions of
+// inv_dct_eo, the same integer result.
+#ifndef P265R_RES_DOT2
+#define P265R_RES_DOT2 1
+#endif
+typedef short res_v2s __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) {          // (int16) lo | (int16) hi << 16
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+template <int N>
+__device__ __forceinline__ void inv_dct_d2(const int (&c)[N], int (&x)[N]) {
+    constexpr int H = N / 2;
+    constexpr int S = 32 / N;
+    int ce[H], ev[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) ce[k] = c[2 * k];
+    if constexpr (H == 2) {
+        ev[0] = kDCT32[0][0] * ce[0] + kDCT32[16][0] * ce[1];
+        ev[1] = kDCT32[0][1] * ce[0] + kDCT32[16][1] * ce[1];
+    } else {
+        inv_dct_d2<H>(ce, ev);
+    }
+    if constexpr (H == 2) {                                      // one odd pair: plain products
+#pragma unroll
+        for (int n = 0; n < H; ++n) {
+            const int od = kDCT32[S][n] * c[1] + kDCT32[3 * S][n] * c[3];
+            x[n] = ev[n] + od;
+            x[N - 1 - n] = ev[n] - od;
+        }
+    } else {
+        uint32_t p[H / 2];                                       // (c[4j+1], c[4j+3])
+#pragma unroll
+        for (int j = 0; j < H / 2; ++j) p[j] = pack16(c[4 * j + 1], c[4 * j + 3]);
+#pragma unroll
+        for (int n = 0; n < H; ++n) {
+            int xp = ev[n];                                      // ev + od accumulated in place (no zero init)
+#pragma unroll
+            for (int j = 0; j < H / 2; ++j) {
+                const uint32_t kk = (uint32_t)(uint16_t)(int16_t)kDCT32[(4 * j + 1) * S][n] |
+                                    (uint32_t)(uint16_t)(int16_t)kDCT32[(4 * j + 3) * S][n] << 16;
+                xp = __builtin_amdgcn_sdot2(__builtin_bit_cast(res_v2s, p[j]), __builtin_bit_cast(res_v2s, kk), xp, false);
+            }
+            x[n] = xp;
+            x[N - 1 - n] = 2 * ev[n] - xp;                       // ev - od
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // NxN, N = 8/16/32: N threads per TB (256/N TBs per 256-thread block).
 //   load row r (16-B vectors) -> dequant -> LDS [r][c]
@@ -209,7 +260,7 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 #pragma unroll
         for (int k = 0; k < N; ++k) e[k] = col[k] << 7;
 #else
-        inv_dct_eo<N>(col, e);
+        if constexpr (P265R_RES_DOT2) inv_dct_d2<N>(col, e); else inv_dct_eo<N>(col, e);
 #endif
 #pragma unroll
         for (int y = 0; y < N; ++y) t[y * S + lane] = (int16_t)clamp16i((e[y] + 64) >> 7);
@@ -223,7 +274,7 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 #pragma unroll
         for (int k = 0; k < N; ++k) xr[k] = row[k];
 #else
-        inv_dct_eo<N>(row, xr);
+        if constexpr (P265R_RES_DOT2) inv_dct_d2<N>(row, xr); else inv_dct_eo<N>(row, xr);
 #endif
         const int bd2 = 20 - bit_depth;
         const int rnd2 = 1 << (bd2 - 1);
