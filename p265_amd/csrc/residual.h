@@ -44,13 +44,15 @@ struct Dequant {
     int scale, lshift, rshift, rnd;
     __device__ __forceinline__ Dequant(int qp, int bd_shift) {
         const int per = qp / 6;
-        scale = 16 * (qp % 6 == 0 ? 40 : qp % 6 == 1 ? 45 : qp % 6 == 2 ? 51 : qp % 6 == 3 ? 57 : qp % 6 == 4 ? 64 : 72);
+        // levelScale[qP % 6] = 40, 45, 51, 57, 64, 72 as the bytes of one 64-bit constant (a shift, not a
+        // per-lane branch tree: qP differs between a wave's TBs)
+        scale = 16 * (int)((0x484039332D28ull >> (8 * (qp - 6 * per))) & 0xffu);
         if (per >= bd_shift) { lshift = per - bd_shift; rshift = 0; rnd = 0; }
         else { lshift = 0; rshift = bd_shift - per; rnd = 1 << (rshift - 1); }
+        scale <<= lshift;                 // <= 1152 << 3 < 2^14: still a 24-bit operand (one v_mad_i32_i24)
     }
     __device__ __forceinline__ int operator()(int level) const {
-        const int p = __mul24(level, scale);
-        return clamp16i(((p << lshift) + rnd) >> rshift);
+        return clamp16i((__mul24(level, scale) + rnd) >> rshift);
     }
 };
 
@@ -172,18 +174,21 @@ typedef short res_v2s __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) {          // (int16) lo | (int16) hi << 16
     return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
 }
+// rnd64: a rounding constant / 64 added to every output for free (folded into the 2-point stage, where every
+// output's sum starts: 64 c0 + 64 c1 + rnd = 64 (c0 + c1 + rnd64))
 template <int N>
-__device__ __forceinline__ void inv_dct_d2(const int (&c)[N], int (&x)[N]) {
+__device__ __forceinline__ void inv_dct_d2(const int (&c)[N], int (&x)[N], int rnd64 = 0) {
     constexpr int H = N / 2;
     constexpr int S = 32 / N;
     int ce[H], ev[H];
 #pragma unroll
     for (int k = 0; k < H; ++k) ce[k] = c[2 * k];
     if constexpr (H == 2) {
-        ev[0] = kDCT32[0][0] * ce[0] + kDCT32[16][0] * ce[1];
-        ev[1] = kDCT32[0][1] * ce[0] + kDCT32[16][1] * ce[1];
+        static_assert(kDCT32[0][0] == 64 && kDCT32[16][0] == 64 && kDCT32[0][1] == 64 && kDCT32[16][1] == -64, "DCT rows 0 / 16");
+        ev[0] = 64 * (ce[0] + ce[1] + rnd64);
+        ev[1] = 64 * (ce[0] - ce[1] + rnd64);
     } else {
-        inv_dct_d2<H>(ce, ev);
+        inv_dct_d2<H>(ce, ev, rnd64);
     }
     if constexpr (H == 2) {                                      // one odd pair: plain products
 #pragma unroll
@@ -260,10 +265,10 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 #pragma unroll
         for (int k = 0; k < N; ++k) e[k] = col[k] << 7;
 #else
-        if constexpr (P265R_RES_DOT2) inv_dct_d2<N>(col, e); else inv_dct_eo<N>(col, e);
+        if constexpr (P265R_RES_DOT2) inv_dct_d2<N>(col, e, 1); else inv_dct_eo<N>(col, e);   // (+64 folded in)
 #endif
 #pragma unroll
-        for (int y = 0; y < N; ++y) t[y * S + lane] = (int16_t)clamp16i((e[y] + 64) >> 7);
+        for (int y = 0; y < N; ++y) t[y * S + lane] = (int16_t)clamp16i((e[y] + (P265R_RES_DOT2 ? 0 : 64)) >> 7);
     }
     __syncthreads();
     if (active) {
@@ -274,7 +279,8 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 #pragma unroll
         for (int k = 0; k < N; ++k) xr[k] = row[k];
 #else
-        if constexpr (P265R_RES_DOT2) inv_dct_d2<N>(row, xr); else inv_dct_eo<N>(row, xr);
+        // (8-bit video: bdShift 12, its rounding 2048 = 64 * 32 folded into the butterfly)
+        if constexpr (P265R_RES_DOT2) inv_dct_d2<N>(row, xr, 1 << (19 - bit_depth - 6)); else inv_dct_eo<N>(row, xr);
 #endif
         const int bd2 = 20 - bit_depth;
         const int rnd2 = 1 << (bd2 - 1);
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int x = v * 8 + h * 2 + q;
-                    r2[q] = clamp16i((xr[x] + rnd2) >> bd2);
+                    r2[q] = clamp16i((xr[x] + (P265R_RES_DOT2 ? 0 : rnd2)) >> bd2);
                 }
                 o[h] = (uint32_t)(uint16_t)r2[0] | ((uint32_t)(uint16_t)r2[1] << 16);
             }
