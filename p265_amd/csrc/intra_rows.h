@@ -176,6 +176,9 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
 #else
 #define P265R_RI(x) (x)
 #endif
+#ifndef P265R_XG_SLEEP
+#define P265R_XG_SLEEP 8                 // s_sleep between the cross-group kernel's progress polls (A/B knob)
+#endif
 #ifndef P265R_XG_PRE
 #define P265R_XG_PRE 0                   // XG: the next CTU's first residual fetched at the publish (A/B knob)
 #endif
@@ -981,7 +984,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             if (__builtin_amdgcn_readfirstlane(XG ? __hip_atomic_load(gptr(err_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                                   : __hip_atomic_load(&ctl.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 return false;                               // (XG: any chain's failure ends every wait)
-            __builtin_amdgcn_s_sleep(P265R_SPIN_SLEEP);   // 64 cycles per unit; each poll costs issue slots
+            __builtin_amdgcn_s_sleep(XG ? P265R_XG_SLEEP : P265R_SPIN_SLEEP);   // 64 cycles per unit; each poll costs issue slots
         }
         __hip_atomic_store(&ctl.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // all lanes, same value
         atomicOr(err_flag, 1);
