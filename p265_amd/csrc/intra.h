@@ -77,6 +77,9 @@ struct Geo {                    // batch-uniform geometry
                                 // take that picture's size from pic_geo().  Per-picture arrays keep the
                                 // context-size slots (CTU records, job counts, maps, planes) -- a
                                 // picture's CTU raster and map rows use ITS width in CTUs / 8x8 blocks
+    int tr_info;                // intra_prep_kernel: compute the top-right / bottom-left job indices (jcount words 1
+                                // and 2) -- set for batches that may run a latency layout (2 pictures per CU or
+                                // fewer), whose row kernels read them; the throughput builds never do
     int tr_check;               // host only: launch the cross-group row kernel's checking instance, which poisons
                                 // the top-right part of a CTU's row-above copy until its wait (checks prep's `tr`
                                 // deterministically; P265R_TR_CHECK, tests)

@@ -432,8 +432,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
             J.w[4] = c.w4; J.w[5] = c.w5 & ~kJ5Bit32;
         }
         if (emit) prep_job_store(jobs + c_out + rank(me_), J);
-        if (tr_c < 0) tr_c = first_of(__ballot(emit && needs_tr(J.w[0], hd, true)), me_, c_out);
-        bl_c = max(bl_c, last_of(__ballot(emit && in_bl(J.w[0], true)), me_, c_out));
+        if (g.tr_info) {                                        // (uniform)
+            if (tr_c < 0) tr_c = first_of(__ballot(emit && needs_tr(J.w[0], hd, true)), me_, c_out);
+            bl_c = max(bl_c, last_of(__ballot(emit && in_bl(J.w[0], true)), me_, c_out));
+        }
         c_out += __popcll(me_);
     }
     int n_out = 0, tr_l = -1, bl_l = -1;
@@ -452,8 +454,10 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const uint32_t w1 = job_w1(l.w0, l.w5, angv);
         const IntraJob J = hd ? make_quad(sj + sq, qb, qc) : luma_job(l, P.zero_off, w1);
         if (emit) prep_job_store(jobs + c_out + n_out + rank(me_), J);
-        if (tr_l < 0) tr_l = first_of(__ballot(emit && needs_tr(J.w[0], hd, false)), me_, n_out);
-        bl_l = max(bl_l, last_of(__ballot(emit && in_bl(J.w[0], false)), me_, n_out));
+        if (g.tr_info) {
+            if (tr_l < 0) tr_l = first_of(__ballot(emit && needs_tr(J.w[0], hd, false)), me_, n_out);
+            bl_l = max(bl_l, last_of(__ballot(emit && in_bl(J.w[0], false)), me_, n_out));
+        }
         n_out += __popcll(me_);
     }
     // per CTU, luma | chroma << 16 each: job counts; the index of the first job that reads the top-right

@@ -522,6 +522,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (const char* v = std::getenv("P265R_FAIR")) g.fair = v[0] != '0';
     g.quad = 3;
     g.tr_check = 0;
+    g.tr_info = 1;
     if (const char* v = std::getenv("P265R_QUAD")) g.quad = std::atoi(v) & 7;
     ctx->n_ctus = g.wc * g.hc;
     // test knobs of the GPU parity matrix (bench.py refuses to run with any P265R_* variable set)
@@ -1027,7 +1028,11 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         // intra job preparation (availability, filter decisions, Cb/Cr pairing): independent
         // of the residuals, timed with the residual phase; enqueued first so that, forked, its
         // waves start before the residual kernels fill the chip
-        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, ctx->prep_lds, ps>>>(b->d_pics, g, b->view);
+        // (a superset of launch_rows' latency layouts: the cross-group kernel and the W = 16 split need
+        // 2 n_pics <= CUs, the experiments' fixed W = 16 any size)
+        Geo gp = g;
+        gp.tr_info = (2 * (long long)b->n_pics <= ctx->num_cus || ctx->row_waves == 16) ? 1 : 0;
+        intra_prep_kernel<<<dim3(g.wc, g.hc, b->n_pics), 64, ctx->prep_lds, ps>>>(b->d_pics, gp, b->view);
         ++tm.residual_launches;
         if (ps != s) HIP_TRY(hipEventRecord(ctx->join_ev[fork_prep == 2 ? 0 : (size_t)b->lane], ps));
         return P265R_OK;
