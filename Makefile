@@ -11,7 +11,14 @@ CXX ?= g++
 FESRC := $(wildcard p265_amd/csrc/fe/*.cpp)
 FEHDR := $(wildcard p265_amd/csrc/fe/*.h) include/p265fe.h include/p265r.h
 
-all: p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so oracle
+# negative-test builds of the half-CTU publish self-checks (tests/test_a_multirank.py): prep places the
+# publish point one job early, with (1) and without (2) prep's own check
+CHECKVARIANTS := p265_amd/libp265r_brbroken1.so p265_amd/libp265r_brbroken2.so
+
+all: p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so $(CHECKVARIANTS) oracle
+
+p265_amd/libp265r_brbroken%.so: $(SRC) $(HDR)
+	$(HIPCC) $(HIPFLAGS) -DP265R_BR_BROKEN=$* -o $@ $(SRC)
 
 # measurement helper (not the product path): the row kernel's job-loop issue ceiling (bench.py)
 p265_amd/libp265probe.so: p265_amd/csrc/issue_probe.hip
@@ -28,7 +35,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so
+	rm -f p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so $(CHECKVARIANTS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

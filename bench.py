@@ -17,7 +17,13 @@ timed region; barriers and the MAX over ranks go over the socket control plane. 
 prints ONE JSON line.
 
     python bench.py                       # N=1, defaults finish in ~1-2 minutes
+    python bench.py --gpus 8              # launches 8 rank processes itself (one per device)
     python -m torch.distributed.run --nproc-per-node 8 bench.py --gpus 8
+
+Without a launcher (WORLD_SIZE unset) and N > 1, this process only spawns the N rank processes
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them) before anything
+touches the GPU, waits for them and exits with the worst return code; rank 0 prints the line.  It
+refuses (exit 2) when WORLD_SIZE differs from --gpus or the ranks need more devices than are visible.
 
 P265R_* environment variables are experiment / test knobs of the library; bench refuses to run
 with any of them set unless --experiment is given (and then records them in the line).
@@ -142,7 +148,7 @@ def issue_ceiling(device, avg_launch_ms, jobs_per_launch, num_cus, rates=None):
     return out
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default c3: 30, c5: 64 -- 16 lanes to fill)")
@@ -174,7 +180,11 @@ def parse():
                     help="N > 1: control plane only, no RCCL communicator (ranks sharing one device: two RCCL "
                          "ranks cannot); the params then travel over the control plane")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run output check (not a headline run)")
-    return ap.parse_args()
+    ap.add_argument("--device-map", default=None,
+                    help="N > 1: comma-separated HIP device of each local rank (default: local rank i on device i); "
+                         "ranks sharing a device need --no-rccl (tests: --gpus 2 --device-map 0,0 --no-rccl)")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive back-end leg")
+    return ap.parse_args(argv)
 
 
 def experiment_env():
@@ -274,25 +284,34 @@ def digest_mismatches(pics, want, got):
     return [i for i, p in enumerate(pics) if not np.array_equal(got[i], want[id(p)])]
 
 
-def verify(ctxs, groups, a, threads, ran=None):
-    """After the timed region: EVERY picture of every resident batch that ran (``ran``: batch slots;
-    with fewer steps than pipeline lanes some never do) through its device digest (p265r_batch_digest,
-    which also reports the sticky row-kernel error word: a dependency give-up in ANY run) against the
-    digest of the C oracle's decode of the same records; and, as a check of the digest itself, the
-    downloaded planes of each batch's first and last pictures (SHA-256 and host digest).
-    -> the line's "verified" object."""
-    from p265_amd import _lib, digest
+def oracle_digests(groups, threads):
+    """Per group: the digest and SHA-256 of the C oracle's decode of every distinct picture
+    ({id(picture): ...}); the reference every device digest is compared with."""
+    from p265_amd import digest
     from oracle import c_oracle
-    n_checked, bad, status_ok, distinct = 0, [], True, set()
-    for (ctx, batches), (params, gp) in zip(ctxs, groups):
+    res = []
+    for params, gp in groups:
         uniq = {}
         for p in gp:
             uniq.setdefault(id(p), p)
         keys = list(uniq)
         ref = c_oracle.decode(params, [uniq[k] for k in keys], threads=threads, with_recon=False)
-        want = {k: digest.picture_digest(r[1]) for k, r in zip(keys, ref)}
-        want_sha = {k: sha_planes(r[1]) for k, r in zip(keys, ref)}
-        distinct |= set(keys)
+        res.append(({k: digest.picture_digest(r[1]) for k, r in zip(keys, ref)},
+                    {k: sha_planes(r[1]) for k, r in zip(keys, ref)}))
+    return res
+
+
+def verify(ctxs, groups, a, wants, ran=None):
+    """After the timed region: EVERY picture of every resident batch that ran (``ran``: batch slots;
+    with fewer steps than pipeline lanes some never do) through its device digest after the batch's
+    final timed run (p265r_batch_digest, which also reports the sticky row-kernel error word: a
+    dependency give-up in ANY run) against the digest of the C oracle's decode of the same records;
+    and, as a check of the digest itself, the downloaded planes of each batch's first and last
+    pictures (SHA-256 and host digest).  -> the line's "verified" object."""
+    from p265_amd import _lib, digest
+    n_checked, bad, status_ok, distinct = 0, [], True, set()
+    for (ctx, batches), (params, gp), (want, want_sha) in zip(ctxs, groups, wants):
+        distinct |= set(want)
         idx = pictures_to_check(len(gp), a.unique if a.workload == "c3" else a.c5_units_per_step)
         for bi, b in enumerate(batches):
             if ran is not None and bi not in ran:
@@ -313,9 +332,44 @@ def verify(ctxs, groups, a, threads, ran=None):
             "batches": sum(1 for _, bs in ctxs for bi in range(len(bs)) if ran is None or bi in ran),
             "status_ok": status_ok, "mismatches": bad[:8],
             "how": "after the timed runs: p265r_batch_digest (device digest of every picture's three output planes, "
-                   "plus the sticky row-kernel error word) of every resident batch that ran, against the digests of "
-                   "oracle/recon_oracle.c's decode of the same records; each batch's first and last pictures are "
-                   "also downloaded and compared by SHA-256 and host digest (p265_amd/digest.py)"}
+                   "plus the sticky row-kernel error word) of every resident batch that ran -- its final timed run -- "
+                   "against the digests of oracle/recon_oracle.c's decode of the same records; each batch's first and "
+                   "last pictures are also downloaded and compared by SHA-256 and host digest (p265_amd/digest.py)"}
+
+
+def checked_pass(ctxs, groups, a, wants, steps):
+    """The timed region's pipelined schedule once more (same batches, lanes and call sequence, so the
+    same row-kernel builds), with a device digest enqueued on the batch's lane after EVERY run
+    (p265r_batch_digest_async, one slot per run): checks each run, not only the last one of every batch,
+    against the oracle.  Not timed.  -> {"runs_checked", "pictures_checked", "ok", "mismatches"}."""
+    from p265_amd import _lib
+    slots = {}
+    for k in range(steps):
+        for ci, (ctx, batches) in enumerate(ctxs):
+            bi = k % a.pipeline
+            s = k // a.pipeline
+            ctx.run(batches[bi])
+            if s < _lib.DIGEST_SLOTS:
+                ctx.digest_async(batches[bi], s)
+                slots[(ci, bi)] = s + 1
+    runs = pics = 0
+    bad = []
+    for (ci, bi), n in sorted(slots.items()):
+        ctx, batches = ctxs[ci]
+        gp = groups[ci][1]
+        want = wants[ci][0]
+        try:
+            got = ctx.digest_slots(batches[bi], n)
+        except _lib.P265RError as e:
+            bad.append("context %d batch %d: %s" % (ci, bi, e))
+            continue
+        for s in range(n):
+            runs += 1
+            pics += len(gp)
+            bad += ["run %d of batch %d picture %d" % (s, bi, i) for i in digest_mismatches(gp, want, got[s])]
+    return {"ok": not bad, "runs_checked": runs, "pictures_checked": pics, "mismatches": bad[:8],
+            "how": "after the timed region, the same %d pipelined steps again with p265r_batch_digest_async after every "
+                   "run (each run's output digest-checked against the oracle before the next run overwrites it)" % steps}
 
 
 def exit_code(out):
@@ -364,6 +418,96 @@ def end_to_end(device, reps=32, threads=16):
             "note": "native front-end (libp265fe.so) on host threads + PCIe-inclusive GPU decode; not `value`"}
 
 
+def stream_ceiling(device):
+    """Achievable HBM stream rates on this box (p265_amd/libp265probe.so p265probe_stream: 16 B per lane,
+    four loads in flight, best grid), the ceiling of the bandwidth-bound phases; hipMemcpyAsync D2D
+    beside it.  GB/s."""
+    import ctypes
+    from p265_amd import hip
+    out = {"memcpy_d2d_gbs": hip.copy_bandwidth_gbs(device)}
+    try:
+        lib = ctypes.CDLL(os.path.join(ROOT, "p265_amd", "libp265probe.so"))
+    except OSError as e:
+        out["error"] = "libp265probe.so: %s" % e
+        return out
+    fn = lib.p265probe_stream
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_double] + [ctypes.POINTER(ctypes.c_double)] * 3
+    c, r, w = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
+    rc = fn(device, float(8 << 30), ctypes.byref(c), ctypes.byref(r), ctypes.byref(w))
+    if rc:
+        out["error"] = "p265probe_stream = %d" % rc
+        return out
+    out.update(copy_gbs=round(c.value, 1), read_gbs=round(r.value, 1), write_gbs=round(w.value, 1),
+               how="16-B-per-lane copy / read / write of 8 GiB buffers, the fastest of a few forms and grids "
+                   "(libp265probe.so p265probe_stream; tools/bw_probe.hip); copy counts read + write bytes")
+    return out
+
+
+def pcie_leg(params, pics, device, steps=3):
+    """The back-end fed over PCIe: per step the batch's records (TB / CTU records + coefficients, the
+    pictures of one c3 step) are uploaded from host memory (p265r_batch_upload: validation, class
+    packing into pinned staging, H2D), run, and every picture's three planes downloaded into host
+    arrays (p265r_batch_download); step k's upload and run overlap step k-1's download on the other
+    lane.  Bytes per direction are what crosses PCIe; the pinned-memory copy rates of the same box
+    stand beside them.  Not `value` (which has the records resident in HBM)."""
+    from p265_amd import hip, recon
+    from p265_amd import records as R
+    # coefficients + TB / CTU records + the 8-B residual job of every coded TB (p265r_batch_upload's H2D copies)
+    h2d_bytes = sum(2 * p.n_coded_coef + R.TB_DTYPE.itemsize * len(p.tbs) + R.CTU_DTYPE.itemsize * len(p.ctus) +
+                    8 * int(((p.tbs["flags"] & R.TB_CBF) != 0).sum()) for p in pics)
+    d2h_bytes = sum(p.meta["samples"] for p in pics)
+    nnz = sum(int(np.count_nonzero(p.coef)) for p in {id(p): p for p in pics}.values())
+    coded = sum(p.n_coded_coef for p in {id(p): p for p in pics}.values())
+    out = {"pictures_per_step": len(pics), "steps": steps}
+    with recon.ReconContext(params, device=device) as ctx:
+        ctx.set_pipeline(2)
+        b = ctx.upload(pics)                    # warm: allocations, pinned staging, kernels
+        ctx.run(b)
+        ctx.download(b)
+        b.free()
+        t0 = time.perf_counter()
+        t_up = t_dl = 0.0
+        prev = None
+        for _ in range(steps):
+            u0 = time.perf_counter()
+            b = ctx.upload(pics)
+            t_up += time.perf_counter() - u0
+            ctx.run(b)
+            if prev is not None:
+                d0 = time.perf_counter()
+                ctx.download(prev)
+                t_dl += time.perf_counter() - d0
+                prev.free()
+            prev = b
+        d0 = time.perf_counter()
+        ctx.download(prev)
+        t_dl += time.perf_counter() - d0
+        prev.free()
+        dt = time.perf_counter() - t0
+    n_ctu = sum(len(p.ctus) for p in pics)
+    out.update(ctu_s=round(n_ctu * steps / dt, 1), ms_per_step=round(dt / steps * 1e3, 2),
+               h2d_mb_per_step=round(h2d_bytes / 1e6, 1), d2h_mb_per_step=round(d2h_bytes / 1e6, 1),
+               h2d_gbs=round(h2d_bytes * steps / t_up / 1e9, 2), d2h_gbs=round(d2h_bytes * steps / t_dl / 1e9, 2),
+               upload_ms_per_step=round(t_up / steps * 1e3, 2), download_ms_per_step=round(t_dl / steps * 1e3, 2),
+               pinned=hip.pinned_copy_gbs(device),
+               coef_nonzero_frac=round(nnz / max(1, coded), 3),
+               note="records uploaded and planes downloaded every step (host <-> HBM over PCIe), kernels as in value; "
+                    "h2d / d2h GB/s = bytes / host wall time of p265r_batch_upload / p265r_batch_download (upload "
+                    "includes host-side validation and class packing)")
+    return out
+
+
+def c5_steps_per_batch(batch_units, units_per_step, world):
+    """K consecutive steps per C5 batch, ONE value for every rank: ceil(batch_units / the largest rank's
+    units per step), so every rank's batch carries its units of the same K steps and the job decodes
+    exactly K x all units per run even when the units do not divide over the ranks (0: one step)."""
+    if batch_units <= 0:
+        return 1
+    max_units = -(-units_per_step // world)
+    return max(1, -(-batch_units // max_units))
+
+
 def build_workload(a, rank, world):
     """-> ([(params, [pictures of this rank with those params])], cpu-baseline sample, config dict).
 
@@ -402,7 +546,9 @@ def build_workload(a, rank, world):
     # distinct pictures); the uneven tiles (1920 x 1088 top, 1920 x 1072 bottom) as ONE ragged batch:
     # one context of the largest tile's size, every unit with its own size (p265r_picture.pic_width /
     # pic_height)
-    k_steps = max(1, -(-a.c5_batch_units // len(units))) if a.c5_batch_units > 0 else 1
+    # one K for every rank (ranks may hold different unit counts when they do not divide): the batch of every
+    # rank carries its units of the same K steps, so the job decodes exactly ctus_all_units x K per run
+    k_steps = c5_steps_per_batch(a.c5_batch_units, 4 * a.c5_frames, sworld)
     step_pics = [tpic for _, tpic, _ in units]
     groups = [(tiles.ragged_params(units), step_pics * k_steps)]
     cols, rows = tiles.tile_grid(p4k, frames[0])
@@ -448,8 +594,101 @@ def c5_unit_latency(ctx, step_pics, runs):
             "note": "one step's %d tile units of this rank as one batch, alone, %d runs" % (len(step_pics), n)}
 
 
-def main():
-    a = parse()
+class Refused(SystemExit):
+    """A command-line / environment combination bench.py will not run (exit 2, message on stderr)."""
+
+    def __init__(self, msg):
+        sys.stderr.write("bench.py: refusing to run: %s\n" % msg)
+        super().__init__(2)
+
+
+def device_map(a, n):
+    """HIP device of each of the n local ranks: --device-map, or local rank i on device i."""
+    if not a.device_map:
+        return list(range(n))
+    try:
+        m = [int(x) for x in a.device_map.split(",")]
+    except ValueError:
+        raise Refused("--device-map %r is not a comma-separated list of device numbers" % a.device_map)
+    if len(m) != n or min(m) < 0:
+        raise Refused("--device-map %r must name one device (>= 0) for each of the %d ranks" % (a.device_map, n))
+    if len(set(m)) < n and not a.no_rccl:
+        raise Refused("ranks sharing a device (--device-map %s) need --no-rccl: two RCCL ranks cannot share one "
+                      "device" % a.device_map)
+    return m
+
+
+def visible_devices():
+    """HIP devices visible to this job, counted in a child process so that THIS process never touches
+    the GPU before it starts the rank processes; -1 when the count fails."""
+    code = ("import sys; sys.path.insert(0, %r)\nfrom p265_amd import hip\ntry:\n    print(hip.device_count())\n"
+            "except hip.HipError:\n    print(0)\n" % ROOT)
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1])
+    except (OSError, subprocess.SubprocessError, ValueError, IndexError):
+        return -1
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv):
+    """bench.py --gpus N without a launcher: start N rank processes of this script (one per device,
+    --device-map), exactly as torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT), wait for all of them and return the worst exit
+    code.  Rank 0 prints the JSON line (inherited stdout).  A rank that fails ends the others after a
+    grace period (they would wait in a barrier for it)."""
+    n = a.gpus
+    dmap = device_map(a, n)
+    vis = visible_devices()
+    if vis < 0:
+        raise Refused("cannot count the visible HIP devices")
+    if max(dmap) + 1 > vis:
+        raise Refused("--gpus %d needs %d HIP device(s) (device map %s), %d visible" % (n, max(dmap) + 1, dmap, vis))
+    port, ctrl = free_port(), free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), P265_CTRL_PORT=str(ctrl))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env, cwd=ROOT))
+    codes, first_fail = [None] * n, None
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None and p.poll() is not None:
+                codes[i] = p.returncode
+                if p.returncode and first_fail is None:
+                    first_fail = time.time()
+        if first_fail is not None and time.time() - first_fail > 60:
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.kill()
+                    codes[i] = p.wait()
+        time.sleep(0.2)
+    worst = 0
+    for c in codes:
+        c = 128 - c if c < 0 else c                          # killed by signal s: 128 + s
+        worst = max(worst, c)
+    if worst:
+        sys.stderr.write("bench.py: rank exit codes %s\n" % codes)
+    return worst
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        raise Refused("--gpus %d" % a.gpus)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)                   # (this process never touches the GPU)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        raise Refused("WORLD_SIZE=%d from the launcher but --gpus %d" % (world_env, a.gpus))
+    dmap = device_map(a, int(os.environ.get("LOCAL_WORLD_SIZE", world_env)))
     c5_latency = a.workload == "c5" and a.c5_batch_units <= 0     # one step per batch, batches side by side
     if a.pipeline is None:
         # 2 lanes: with the prep stream of each lane, 4 streams on HIP's default 4 hardware queues, one
@@ -479,13 +718,16 @@ def main():
     from p265_amd import dist, hip, recon
 
     host = host_info()
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     # pure-Python CPU baseline first, in a child process, before this process touches the GPU
     py_base = None
     if world_env == 1 and not a.no_cpu_baseline and a.workload == "c3":
         py_base = cpu_baseline_python(host["cpu_share"])
-    rank, world, local = dist.init(device=int(os.environ.get("LOCAL_RANK", "0")),
-                                   rccl=world_env > 1 and not a.no_rccl)
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if local_rank >= len(dmap):
+        raise Refused("LOCAL_RANK %d outside the device map %s" % (local_rank, dmap))
+    rank, world, _ = dist.init(device=dmap[local_rank], rccl=world_env > 1 and not a.no_rccl)
+    local = dmap[local_rank]                               # this rank's HIP device
+    rccl_ranks = dist.rccl_ranks()                         # ncclCommCount of every rank (None: no RCCL)
 
     t0 = time.time()
     groups, (cpu_params, cpu_sample, cpu_what), cfg = build_workload(a, rank, world)
@@ -517,6 +759,7 @@ def main():
     for k in range(a.warmup):
         step(k)
     sync_all()
+    builds0 = [ctx.describe()["row_launches"] for ctx, _ in ctxs]
     dist.barrier()
     t_start = time.perf_counter()
     for k in range(a.steps):               # queued back to back, batches alternating over the streams
@@ -525,6 +768,12 @@ def main():
     elapsed_local = time.perf_counter() - t_start
     dist.barrier()
     elapsed = dist.max_over_ranks(elapsed_local)
+    # which row-kernel build the timed steps ran (p265r_describe row_launches, difference over the region)
+    builds_timed = {}
+    for (ctx, _), b0 in zip(ctxs, builds0):
+        for k, v in ctx.describe()["row_launches"].items():
+            if v - b0[k]:
+                builds_timed[k] = builds_timed.get(k, 0) + v - b0[k]
     # phase breakdown + roofline: the same steps on ONE batch per context (one stream, no
     # overlap, contexts one after another), HIP events around each phase, so every kernel's
     # duration is its own
@@ -540,6 +789,20 @@ def main():
         acc = t if acc is None else {k: acc[k] + t[k] for k in acc}
     knobs = ctxs[0][0].describe()
     jl, jch = ctxs[0][0].job_count(ctxs[0][1][0])
+    # the pipelined steps' row kernel after the first is the W = 8 build (beside the other lane's phases):
+    # the same batch alone through that build, so the line carries both builds' isolated launch times
+    w8 = None
+    if a.workload == "c3" and acc["intra_launches"] == a.steps:
+        ctx0, b0 = ctxs[0][0], ctxs[0][1][0]
+        ctx0.set_row_waves(8)
+        ctx0.set_timing(True)
+        for _ in range(a.steps):
+            ctx0.run(b0)
+        ctx0.sync()
+        ctx0.set_timing(False)
+        ctx0.set_row_waves(0)
+        t8 = ctx0.timings_total()
+        w8 = t8["intra_ms"] / max(1, t8["intra_launches"])
 
     if a.workload == "c3":
         total_ctus = world * n_ctu * a.steps
@@ -568,10 +831,10 @@ def main():
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
                                         % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
-                     "note": "bound by instruction issue (the CU's one scalar unit + each SIMD's VALU shared by "
-                             "24 waves; waves park on s_waitcnt 42 % of their cycles while others issue), not by "
-                             "HBM: halving the quad jobs' LDS round trips at +10-15 % instructions was 18 % slower "
-                             "(DESIGN.md §4, round 4); see issue_rates"},
+                     "note": "achieved / avg_launch_ms: the batch alone, which runs the W = 12 build; the pipelined steps "
+                             "run W = 8 after their first (builds).  Bound by instruction issue (the CU's one scalar "
+                             "unit + each SIMD's VALU shared by 24 waves; waves park on s_waitcnt 42 % of their cycles "
+                             "while others issue), not by HBM (DESIGN.md §4); see issue_rates"},
         "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms),
         "intra_jobs_per_launch": {"luma": jl, "chroma": jch},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
@@ -580,6 +843,12 @@ def main():
                       "whole_path_algorithmic": round(tot_b / (elapsed / a.steps) / 1e9, 2)},
         "setup_s": round(gen_s, 1),
     }
+    builds = {"timed_steps_launches": builds_timed,
+              "w12_alone": {"avg_launch_ms": round(avg_launch_ms, 4), "frac": round(achieved / HBM_PEAK_GBS, 4)}}
+    if w8:
+        builds["w8_alone"] = {"avg_launch_ms": round(w8, 4),
+                              "frac": round(bytes_per_launch / (w8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    out["roofline"]["builds"] = builds
     if a.workload == "c5":
         out["unit_latency_ms"] = c5_unit_latency(ctxs[0][0], cpu_sample, a.steps)
         if a.c5_world:
@@ -590,16 +859,26 @@ def main():
     if exp:
         out["experiment_env"] = exp
     if world > 1:
-        out["collectives"] = ("control plane only (--no-rccl)" if a.no_rccl else
-                              "ncclBroadcast of the 32-B params (RCCL); barriers + MAX over the control plane")
+        out["collectives"] = {"kind": ("control plane only (--no-rccl)" if a.no_rccl else
+                                       "ncclBroadcast of the 32-B params (RCCL); barriers + MAX over the control plane"),
+                              "rccl_ranks": rccl_ranks, "devices": dist.allgather_json(local),
+                              "launcher": "torch.distributed.run or bench.py's own (--gpus N, WORLD_SIZE unset)"}
     if not a.no_verify:
-        v = verify(ctxs, groups, a, host["cpu_share"], ran)
+        wants = oracle_digests(groups, host["cpu_share"])
+        v = verify(ctxs, groups, a, wants, ran)
+        cp = checked_pass(ctxs, groups, a, wants, a.steps)
+        v["every_run"] = cp
+        v["ok"] = v["ok"] and cp["ok"]
         # every rank checks its own batches; the job is ok only if all are
         v["ranks_failed"] = int(dist.max_over_ranks(0.0 if v["ok"] else 1.0)) if world > 1 else int(not v["ok"])
         v["ok"] = v["ok"] and v["ranks_failed"] == 0
         out["verified"] = v
     if rank == 0:
-        out["roofline"]["achievable_copy_gbs"] = hip.copy_bandwidth_gbs(local)
+        sc = stream_ceiling(local)
+        out["roofline"]["achievable"] = sc
+        ceil = sc.get("copy_gbs") or sc["memcpy_d2d_gbs"]
+        out["phase_gbs"]["vs_achievable_copy"] = {k: round(v / ceil, 3) for k, v in out["phase_gbs"].items()
+                                                  if isinstance(v, float) and k != "whole_path_algorithmic"}
         if a.workload == "c3" and launches_per_step == 1:
             out["roofline"]["issue"] = issue_ceiling(local, avg_launch_ms, jl + jch,
                                                      int(knobs.get("num_cus", 256)), out["issue_rates"])
@@ -615,6 +894,8 @@ def main():
         for b in batches:
             b.free()
         ctx.close()
+    if rank == 0 and world == 1 and not a.no_pcie and a.workload == "c3":
+        out["pcie"] = pcie_leg(groups[0][0], groups[0][1], local)
     if rank == 0 and world == 1 and not a.no_e2e and a.workload == "c3":
         out["end_to_end"] = end_to_end(local, threads=min(16, host["cpu_share"]))
     if rank == 0:

@@ -182,6 +182,15 @@ int  p265r_batch_status(p265r_ctx* ctx, p265r_batch* batch);
  * n = 3 * the batch's pictures.  Returns what p265r_batch_status returns afterwards.  Lets a
  * benchmark check every picture it timed.  No counterpart in the reference. */
 int  p265r_batch_digest(p265r_ctx* ctx, p265r_batch* batch, int which, uint64_t* out, int n);
+/* The same digest ENQUEUED on the batch's lane after every run enqueued so far, into slot `slot`
+ * (0 .. P265R_DIGEST_SLOTS-1) of the batch's digest buffer; returns without waiting (the buffer is
+ * allocated at the first call).  p265r_batch_digest_slots waits for the lane and copies slots
+ * [0, n_slots): out[(s * n_pics + i) * 3 + c].  Lets a caller check EVERY run of a pipelined schedule,
+ * not only the last (a run's output is otherwise overwritten by the batch's next run).  A slot
+ * written twice holds the later digest.  No counterpart in the reference. */
+#define P265R_DIGEST_SLOTS 64
+int  p265r_batch_digest_async(p265r_ctx* ctx, p265r_batch* batch, int which, int slot);
+int  p265r_batch_digest_slots(p265r_ctx* ctx, p265r_batch* batch, uint64_t* out, int n_slots);
 /* Intra jobs of the batch's last run (after job preparation: a 4x4 quad counts once, a Cb+Cr pair
  * once), luma and chroma, summed over its pictures; waits for the batch's lane.  For measurement
  * (bench.py: the row kernel's cycles per job).  No counterpart in the reference. */
@@ -205,6 +214,11 @@ int  p265r_sync(p265r_ctx* ctx);
  * runtime accepts at most 32, so past depth 15 such batches share hardware queues).
  * Runs of one batch stay ordered; p265r_sync waits for every stream.  Default 1. */
 int  p265r_set_pipeline(p265r_ctx* ctx, int depth);
+/* Measurement knob (no counterpart in the reference): force the intra row kernel's build for this
+ * context's later runs -- 8 or 12 waves per workgroup -- or 0 (default) to pick it per run (12 for a
+ * batch alone, 8 beside other lanes' runs, the latency layouts for small batches).  Lets a benchmark
+ * time the build its pipelined steps run, in isolation. */
+int  p265r_set_row_waves(p265r_ctx* ctx, int waves);
 /* Enable (1, which also starts a new accumulation) / disable (0) per-phase HIP-event
  * timing of every p265r_batch_run; read the last run's timings, or the sums over all runs
  * since enabling (runs may be queued back to back: nothing here waits per run). */

@@ -18,6 +18,8 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("P265R_LIB", os.path.join(HERE, "libp265r.so"))
 
+DIGEST_SLOTS = 64                # P265R_DIGEST_SLOTS
+
 # error codes (include/p265r.h)
 OK, EINVAL, ENOMEM, EHIP, EUNSUPPORTED, ERANGE, ESTATE, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
 
@@ -73,12 +75,15 @@ SIGNATURES = {
     "p265r_batch_download": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(PictureC), ctypes.c_int]),
     "p265r_batch_status": (ctypes.c_int, [_vp, _vp]),
     "p265r_batch_digest": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "p265r_batch_digest_async": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
+    "p265r_batch_digest_slots": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "p265r_batch_job_count": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "p265r_batch_free": (ctypes.c_int, [_vp, _vp]),
     "p265r_submit": (ctypes.c_int, [_vp, ctypes.POINTER(PictureC), ctypes.c_int]),
     "p265r_wait": (ctypes.c_int, [_vp]),
     "p265r_sync": (ctypes.c_int, [_vp]),
     "p265r_set_pipeline": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "p265r_set_row_waves": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265r_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265r_last_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
     "p265r_timings_total": (ctypes.c_int, [_vp, ctypes.POINTER(Timings), ctypes.POINTER(ctypes.c_int)]),

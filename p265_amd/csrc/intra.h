@@ -56,6 +56,8 @@ struct BatchView {
     uint64_t pic_bytes;         // bytes of one picture's three planes
     uint64_t plane_off[3];      // Y, Cb, Cr offsets inside a picture's planes
     const p265r_ctu* ctus0;     // picture 0's CTU records (PicSizeInCtbsY per picture)
+    int* err;                   // the batch's sticky error word (bit 0: a row-kernel wait gave up; bit 1: the
+                                // prep kernel's half-CTU self-check failed, Geo::tr_check)
 };
 
 struct Geo {                    // batch-uniform geometry
@@ -80,9 +82,11 @@ struct Geo {                    // batch-uniform geometry
     int tr_info;                // intra_prep_kernel: compute the top-right / bottom-left job indices (jcount words 1
                                 // and 2) -- set for batches that may run a latency layout (2 pictures per CU or
                                 // fewer), whose row kernels read them; the throughput builds never do
-    int tr_check;               // host only: launch the cross-group row kernel's checking instance, which poisons
-                                // the top-right part of a CTU's row-above copy until its wait (checks prep's `tr`
-                                // deterministically; P265R_TR_CHECK, tests)
+    int tr_check;               // P265R_TR_CHECK (tests): the host launches the cross-group row kernel's checking
+                                // instance, which poisons the top-right part of a CTU's row-above copy until its
+                                // wait and serves the left half of every CTU's bottom line from the half-CTU
+                                // publish alone (checks prep's `tr` and `br` deterministically); the prep kernel
+                                // checks `br` against the TBs' extents (error word bit 1)
 };
 
 // A/B: s_setprio of the bandwidth-phase kernels' waves (residual, prep, SAO), 0 = default

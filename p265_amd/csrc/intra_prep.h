@@ -403,13 +403,22 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         const int hq = chroma ? ctb >> 2 : ctb >> 1;
         return ((int)(o & (chroma ? 31u : 63u)) < hq) & ((int)(o >> (chroma ? 5 : 6)) >= hq);
     };
+    // self-check of `br` (Geo::tr_check, tests): does a job's EXTENT cover a sample of the bottom row of the
+    // CTB's left half?  (Independent of in_bl's origin rule.)  No such job may come at or after `br`.
+    auto touches_bl_row = [&](uint32_t w0, bool quad, bool chroma) -> bool {
+        const uint32_t o = (w0 & 0x1fffu) - (chroma ? 4096u : 0u);
+        const int cts = chroma ? ctb >> 1 : ctb;
+        const int xr = (int)(o & (chroma ? 31u : 63u)), yr = (int)(o >> (chroma ? 5 : 6));
+        const int ext = quad ? 8 : 4 << ((w0 >> 13) & 3u);
+        return (xr < cts / 2) & (yr + ext >= cts);
+    };
     auto last_of = [&](unsigned long long m, unsigned long long me, int out) {    // index of m's last job
         return m ? out + (int)__popcll(me & ((2ull << (63 - __clzll((long long)m))) - 1ull)) - 1 : -1;
     };
     auto first_of = [&](unsigned long long m, unsigned long long me, int out) {   // index of m's first job
         return m ? out + (int)__popcll(me & ((1ull << (__ffsll((long long)m) - 1)) - 1ull)) : -1;
     };
-    int c_out = 0, tr_c = -1, bl_c = -1;
+    int c_out = 0, tr_c = -1, bl_c = -1, tb_c = -1;
     unsigned long long hp = 0;
     for (int base = 0; base < n_chroma; base += 64) {
         const int s = base + lane;
@@ -435,10 +444,11 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         if (g.tr_info) {                                        // (uniform)
             if (tr_c < 0) tr_c = first_of(__ballot(emit && needs_tr(J.w[0], hd, true)), me_, c_out);
             bl_c = max(bl_c, last_of(__ballot(emit && in_bl(J.w[0], true)), me_, c_out));
+            if (g.tr_check) tb_c = max(tb_c, last_of(__ballot(emit && touches_bl_row(J.w[0], hd, true)), me_, c_out));
         }
         c_out += __popcll(me_);
     }
-    int n_out = 0, tr_l = -1, bl_l = -1;
+    int n_out = 0, tr_l = -1, bl_l = -1, tb_l = -1;
     hp = 0;
     for (int base = 0; base < n_luma; base += 64) {
         const int s = base + lane;
@@ -457,9 +467,21 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
         if (g.tr_info) {
             if (tr_l < 0) tr_l = first_of(__ballot(emit && needs_tr(J.w[0], hd, false)), me_, n_out);
             bl_l = max(bl_l, last_of(__ballot(emit && in_bl(J.w[0], false)), me_, n_out));
+            if (g.tr_check) tb_l = max(tb_l, last_of(__ballot(emit && touches_bl_row(J.w[0], hd, false)), me_, n_out));
         }
         n_out += __popcll(me_);
     }
+#ifdef P265R_BR_BROKEN      // negative test of the half-CTU publish checks: publish before the last bottom-left job
+    const int br_l = bl_l < 0 ? n_out : bl_l, br_c = bl_c < 0 ? c_out : bl_c;
+#else
+    const int br_l = bl_l < 0 ? n_out : bl_l + 1, br_c = bl_c < 0 ? c_out : bl_c + 1;
+#endif
+    // a job covering the bottom row's left half at or after `br` would leave the half-CTU publish stale
+    // (P265R_BR_BROKEN=2: the broken `br` without this check, so the row kernel's poisoned half line alone
+    // must catch it)
+#if !(defined(P265R_BR_BROKEN) && P265R_BR_BROKEN == 2)
+    if (g.tr_check && lane == 0 && (tb_l >= br_l || tb_c >= br_c)) atomicOr(v.err, 2);
+#endif
     // per CTU, luma | chroma << 16 each: job counts; the index of the first job that reads the top-right
     // CTU (= the count when none does); one past the last job in the bottom-left quadrant (= the count when
     // there is none: a CTU row below the picture's last sample row has no reader)
@@ -472,7 +494,7 @@ __global__ __launch_bounds__(64) void intra_prep_kernel(const DevPic* __restrict
 #else
                (uint32_t)(tr_l < 0 ? n_out : tr_l) | (uint32_t)(tr_c < 0 ? c_out : tr_c) << 16,
 #endif
-               (uint32_t)(bl_l < 0 ? n_out : bl_l + 1) | (uint32_t)(bl_c < 0 ? c_out : bl_c + 1) << 16, 0u};
+               (uint32_t)br_l | (uint32_t)br_c << 16, 0u};
     }
 }
 

@@ -887,15 +887,18 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
 // fit beside it on every SIMD (p265r.hip launch_rows; measured in DESIGN.md §6).
 //
 // XG (cross-group chains, the latency regime): every picture's luma chain and chroma chain each run on
-// `xg` workgroups of W waves (W = 4: one wave per SIMD, on xg CUs), rows dealt statically (wave k of the
-// chain's xg * W runs rows k, k + xg W, ...); row progress and the rows' bottom lines live in global
-// memory (XgBuf), read and written with agent-scope atomics (coherent across the XCDs' L2s), and a
-// CTU's row above is copied from there into the wave's ytop / ctop.  One line per CTU row (no parity
-// reuse): a CTU's publish never waits for the row below to have read the line.
+// `xg` workgroups of W waves (W = 4: one wave per SIMD, on xg CUs); a wave claims its chain's next row
+// from a global ticket (one atomic per row, taken only by a running wave), so a row's predecessor is
+// always held by a wave that already runs, whatever part of the chain's workgroups the dispatcher has
+// placed (other lanes' or contexts' kernels may hold the rest of the GPU); row progress and the rows'
+// bottom lines live in global memory (XgBuf), read and written with agent-scope atomics (coherent across
+// the XCDs' L2s), and a CTU's row above is copied from there into the wave's ytop / ctop.  One line per
+// CTU row (no parity reuse): a CTU's publish never waits for the row below to have read the line.
 struct XgBuf {
     int* prog;                   // [pic][comp][row]: seq << 16 | CTUs done
     uint8_t* lines;              // [pic][comp][row][(wc + 2) * CTB]: the row's bottom samples at + CTB
                                  // (chroma: Cb at + CTB / 2, Cr (wc + 2) * CTB / 2 further)
+    int* ticket;                 // [pic][comp]: the chain's next unclaimed row (cleared per run with prog)
     int xg, seq;                 // workgroups per chain; this run's tag
 };
 
@@ -960,9 +963,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     const int split_comp = (int)(blockIdx.x & 1u);
     const int n_my = b < n_pics ? (n_pics - b + G - 1) / G : 0;
     const int rows_total = XG ? g.hc : n_my * units;
-    // XG: this workgroup's chain (picture, component) and its first wave's index in the chain
+    // XG: this workgroup's chain (picture, component)
     const int xg_chain = XG ? (int)blockIdx.x / xb.xg : 0;
-    const int xg_wave = XG ? ((int)blockIdx.x - xg_chain * xb.xg) * W + wave : 0;
     const size_t xg_row_bytes = (size_t)(g.wc + 2) << g.ctb_log2;
     const int ctb = 1 << g.ctb_log2;
     // bounded spin-wait on an LDS word; false = gave up (error published, caller bails out).
@@ -993,14 +995,15 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     bool failed = false;
 
     P265R_TRACE(1);
-    int xg_next = xg_wave;                                 // XG: this wave's next row
     for (;;) {
         // row queue: the whole wave executes the atomic (no lane-0 branch inside the loop);
         // only lane 0 contributes, so the wave takes exactly one row
         int r;
         if constexpr (XG) {
-            r = xg_next;
-            xg_next += xb.xg * W;
+            // the chain's global ticket (the rows of a chain are claimed in order by running waves)
+            r = __hip_atomic_fetch_add(gptr_w(xb.ticket) + xg_chain, lane == 0 ? 1 : 0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            r = __builtin_amdgcn_readlane(r, 0);
         } else {
             r = __hip_atomic_fetch_add(&ctl.next_row, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1275,6 +1278,17 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             // the top-right wait before job tr (the row above the CTU suffices for the jobs before it)
             const int t_trw = tr_done || tr >= nt ? -1 : tr;
             const int t_half = halfp && br < nt ? br : -1;     // XG: publish the bottom row's left half first
+            if (TRCHK && t_half >= 0) {
+                // self-check of prep's `br`: the bottom row's left half starts poisoned (no job reads it before
+                // writing it: unavailable samples) and the CTU's final publish leaves that half of the line to
+                // the half-CTU publish alone, so a bottom-left job placed after `br` breaks parity on every run
+                const int h = comp ? lane >> 5 : 0, k = comp ? lane & 31 : lane;
+                const int hv = min(cts, (comp ? ph >> 1 : ph) - (y0 >> comp));
+                if (k < cts / 8)
+                    *reinterpret_cast<uint32_t*>((comp ? L.c[h] : L.y) + (hv - 1) * (comp ? 32 : 64) + 4 * k) =
+                        0x3cc3a55au ^ (uint32_t)((cx * 64 + k) * 0x01030507);
+                wave_sync();
+            }
 #ifdef P265R_JOB_UNROLL
 #pragma unroll P265R_JOB_UNROLL
 #endif
@@ -1436,7 +1450,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 }
                 if constexpr (XG) {                            // bottom row, whole dwords (past the edge: unread)
                     P265R_GLOBAL uint8_t* dl = xg_line + (size_t)cy * xg_row_bytes + (c == 2 ? xg_row_bytes >> 1 : 0) + cs + xb;
-                    if (lane < cs / 4)
+                    // (the check instance: the left half stays what the half-CTU publish wrote)
+                    if (lane < cs / 4 && !(TRCHK && t_half >= 0 && lane < cs / 8))
                         __hip_atomic_store(reinterpret_cast<P265R_GLOBAL uint32_t*>(dl) + lane,
                                            *reinterpret_cast<const uint32_t*>(src + (hv - 1) * ist + 4 * lane),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

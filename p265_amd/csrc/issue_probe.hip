@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace {
 
 template <int V, int S, int L>
@@ -83,22 +85,87 @@ int run(int device, int jobs, double* cycles_per_job_cu, double* ms) {
     return 0;
 }
 
+// ---- achievable HBM stream rates (bench.py roofline.achievable): 16 B per lane; the fastest of a few
+// copy / read / write forms and grids measured on the box (tools/bw_probe.hip: grid-stride plain copy at
+// 8-32 workgroups per CU, one contiguous chunk per workgroup with 4 loads in flight per lane at 1-4 per
+// CU; non-temporal stores for the write).  What the bandwidth-bound phases (residual, SAO) are compared
+// against; the guide quotes 6.29 TB/s for a float4 copy (MI355X_MICROARCH.md).
+typedef unsigned int probe_u4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void copy_probe_kernel(const probe_u4* __restrict__ a, probe_u4* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) b[i] = a[i];
+}
+__global__ __launch_bounds__(256) void copy_chunk_probe_kernel(const probe_u4* __restrict__ a, probe_u4* __restrict__ b,
+                                                               size_t n, size_t per) {
+    const size_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+    for (size_t i = lo + threadIdx.x; i < hi; i += 256 * 4) {
+        probe_u4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (i + 256 * u < hi) x[u] = a[i + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (i + 256 * u < hi) b[i + 256 * u] = x[u];
+    }
+}
+__global__ __launch_bounds__(256) void read_probe_kernel(const probe_u4* __restrict__ a, probe_u4* __restrict__ sink, size_t n) {
+    probe_u4 acc = {0u, 0u, 0u, 0u};
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) acc ^= a[i];
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[threadIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void write_probe_kernel(probe_u4* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        __builtin_nontemporal_store(probe_u4{1u, 2u, 3u, (unsigned)i}, b + i);
+}
+
 }  // namespace
 
 extern "C" {
 
-// which: 0 = the round-5 row-kernel mix (VALU 131, SALU 81, LDS 15 per job), 1 = its VALU alone,
-// 2 = its SALU alone, 3 = its LDS alone.  -> CU-cycles per job (s_memtime, the slowest wave) and the
-// launch time.  Returns 0, or < 0 on a HIP error.
-int p265probe_issue(int device, int which, int jobs, double* cycles_per_job_cu, double* ms) {
-    if (!cycles_per_job_cu || !ms || jobs < 8) return -1;
-    switch (which) {
-        case 0: return run<131, 81, 15>(device, jobs, cycles_per_job_cu, ms);
-        case 1: return run<131, 0, 0>(device, jobs, cycles_per_job_cu, ms);
-        case 2: return run<0, 81, 0>(device, jobs, cycles_per_job_cu, ms);
-        case 3: return run<0, 0, 15>(device, jobs, cycles_per_job_cu, ms);
-        default: return -1;
+// Best rate over the forms above (5 timed repetitions each, after one warm-up) of a copy (read + write
+// bytes), a read and a write of `bytes`-sized buffers, in GB/s.  Returns 0, or < 0 on a HIP error /
+// allocation failure.
+int p265probe_stream(int device, double bytes, double* copy_gbs, double* read_gbs, double* write_gbs) {
+    if (!copy_gbs || !read_gbs || !write_gbs || bytes < (1 << 20)) return -1;
+    if (hipSetDevice(device) != hipSuccess) return -3;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -3;
+    const size_t nb = (size_t)bytes / 16 * 16, n = nb / 16;
+    probe_u4 *a = nullptr, *b = nullptr;
+    if (hipMalloc(&a, nb) != hipSuccess) return -2;
+    if (hipMalloc(&b, nb) != hipSuccess) { (void)hipFree(a); return -2; }
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipError_t e = hipMemset(a, 1, nb);
+    if (e == hipSuccess) e = hipMemset(b, 0, nb);
+    double best[3] = {0, 0, 0};
+    // (kind, workgroups per CU): copy plain 8 / 16 / 32, copy chunked 1 / 2 / 4, read 8 / 16 / 32, write 4 / 8 / 16
+    const int forms[12][2] = {{0, 8}, {0, 16}, {0, 32}, {1, 1}, {1, 2}, {1, 4}, {2, 8}, {2, 16}, {2, 32}, {3, 4}, {3, 8}, {3, 16}};
+    for (int f = 0; f < 12 && e == hipSuccess; ++f) {
+        const int kind = forms[f][0], grid = forms[f][1] * cus;
+        const size_t per = (n + grid - 1) / grid;
+        for (int rep = 0; rep < 6 && e == hipSuccess; ++rep) {
+            (void)hipEventRecord(e0, nullptr);
+            switch (kind) {
+                case 0: copy_probe_kernel<<<grid, 256>>>(a, b, n); break;
+                case 1: copy_chunk_probe_kernel<<<grid, 256>>>(a, b, n, per); break;
+                case 2: read_probe_kernel<<<grid, 256>>>(a, b, n); break;
+                default: write_probe_kernel<<<grid, 256>>>(b, n); break;
+            }
+            (void)hipEventRecord(e1, nullptr);
+            e = hipEventSynchronize(e1);
+            float ms = 0;
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+            const int k = kind <= 1 ? 0 : kind - 1;
+            const double moved = (k == 0 ? 2.0 : 1.0) * (double)nb;
+            if (e == hipSuccess && rep > 0 && ms > 0) best[k] = std::max(best[k], moved / (ms * 1e-3) / 1e9);
+        }
     }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    if (e != hipSuccess) return -3;
+    *copy_gbs = best[0]; *read_gbs = best[1]; *write_gbs = best[2];
+    return 0;
 }
 
 }  // extern "C"

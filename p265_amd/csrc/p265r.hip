@@ -137,6 +137,8 @@ struct p265r_ctx {
     int xg = 4;                // workgroups per chain of the cross-group row kernel (P265R_XG; 0: off; launch_rows)
     bool last_split = false;   // the last row-kernel launch was split (p265r_describe)
     bool last_xg = false;      // ... was the cross-group kernel
+    long long row_launches[5] = {0, 0, 0, 0, 0};   // row-kernel launches per build: W = 12, W = 8, W = 16 split,
+                                                   // cross-group, other (experiments) -- p265r_describe
     int luma_lead = -1;        // rows the luma chain leads the chroma chain in the row queue (P265R_LUMA_LEAD);
                                // -1 = by run: 8 for a batch alone, 5 beside other lanes' batches (round 3,
                                // 2 reps: alone lead 5/7/8/10 -> 4.28/4.23/4.19/4.22 ms, pipelined
@@ -208,6 +210,7 @@ struct p265r_batch {
     int runs = 0;              // p265r_batch_run calls so far
     hipEvent_t sao_done = nullptr;     // P265R_SAO_AUX: recorded on the aux stream after a run's loop filters
     bool sao_pending = false;          // ... and not yet joined into the lane stream (join_sao)
+    unsigned long long* d_dig = nullptr;   // p265r_batch_digest_async slots: P265R_DIGEST_SLOTS x n_pics x 3
     hipEvent_t intra_done = nullptr;   // recorded after each run's intra phase (the last reader of the
                                        // residual pool and job lists): the next run's residual + prep
                                        // phase waits for it instead of for the whole previous run
@@ -402,7 +405,8 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     // per CU, no workgroup starts after another ends) -- and only worth it for a batch alone
     g.fair = g.fair && alone && per_cu == 2 && !split;
     // (XG: the progress words were cleared with the CU slots this run, so one tag serves every run)
-    const XgBuf xb{XG ? b->d_xg_prog : nullptr, XG ? b->d_xg_lines : nullptr, XG ? ctx->xg : 0, 1};
+    const XgBuf xb{XG ? b->d_xg_prog : nullptr, XG ? b->d_xg_lines : nullptr,
+                   XG ? b->d_xg_prog + 2 * (size_t)g.hc * b->n_pics : nullptr, XG ? ctx->xg : 0, 1};
     g.ragged = b->ragged ? 1 : 0;
     int* dbg = nullptr;
 #ifdef P265R_DEBUG_DIAG
@@ -416,6 +420,7 @@ int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     fn<<<grid, 64 * W, lds, st>>>(b->d_pics, b->d_pool, b->d_res, g, b->n_pics, fs, lead, b->d_err, dbg, split ? 1 : 0, xb);
     ctx->last_split = split;
     ctx->last_xg = XG;
+    ++ctx->row_launches[XG ? 3 : (W == 16 ? 2 : (W == 8 ? 1 : (W == 12 ? 0 : 4)))];
     HIP_TRY(hipGetLastError());
 #ifdef P265R_DEBUG_DIAG
     if (dbg) {
@@ -702,7 +707,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     // cross-group row kernel (a batch whose chains fit xg workgroups each on the CUs): its progress words
     // follow the CU slots (cleared together per run), its lines get their own range
     const bool xg_ok = ctx->xg > 0 && ctx->split && 2 * (long long)n_pics * ctx->xg <= ctx->num_cus;
-    const size_t xg_prog_bytes = xg_ok ? sizeof(int) * 2 * (size_t)g.hc * n_pics : 0;
+    // (+ one row ticket per chain)
+    const size_t xg_prog_bytes = xg_ok ? sizeof(int) * 2 * ((size_t)g.hc + 1) * n_pics : 0;
     const size_t o_err = off; off = align_up(off + 256 + kRowCuSlots * 16 + xg_prog_bytes, 256);
     const size_t o_xgl = off;
     if (xg_ok) off = align_up(off + 2 * (size_t)g.hc * ((size_t)(g.wc + 2) << g.ctb_log2) * n_pics, 256);
@@ -881,6 +887,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->view.plane_off[1] = align_up(plane_bytes[0], 256);
     b->view.plane_off[2] = b->view.plane_off[1] + align_up(plane_bytes[1], 256);
     b->view.ctus0 = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus);
+    b->view.err = b->d_err;
     std::memset(host + o_err, 0, o_ctus - o_err);                                        // error word
     // alignment gaps between the arrays: zero, as the device image always had them
     {
@@ -1081,7 +1088,7 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         // per-CU workgroup slots cleared per run; the error word (d_err[0]) is sticky from upload on,
         // so p265r_batch_status / p265r_batch_download report a give-up in ANY run of the batch
         // (and the cross-group kernel's progress words behind them)
-        HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16 + (b->d_xg_prog ? sizeof(int) * 2 * (size_t)g.hc * b->n_pics : 0), s));
+        HIP_TRY(hipMemsetAsync(b->d_err + 64, 0, kRowCuSlots * 16 + (b->d_xg_prog ? sizeof(int) * 2 * ((size_t)g.hc + 1) * b->n_pics : 0), s));
         // the previous run's loop filters (on the aux stream) read the planes this run writes
         if (b->sao_pending) { HIP_TRY(hipStreamWaitEvent(s, b->sao_done, 0)); b->sao_pending = false; }
         if (ordered && ctx->last_lf_valid) HIP_TRY(hipStreamWaitEvent(s, ctx->last_lf_ev, 0));
@@ -1271,7 +1278,9 @@ int p265r_batch_status(p265r_ctx* ctx, p265r_batch* b) {
     int err = 0;
     HIP_TRY(hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
-        g_last_hip_error = "intra row pipeline: dependency wait timed out";
+        g_last_hip_error = (err & 1) ? "intra row pipeline: dependency wait timed out"
+                                     : "job prep self-check (P265R_TR_CHECK): a job covering the bottom row's left half "
+                                       "comes after the half-CTU publish point";
         return P265R_EHIP;
     }
     return P265R_OK;
@@ -1294,6 +1303,35 @@ int p265r_batch_digest(p265r_ctx* ctx, p265r_batch* b, int which, uint64_t* out,
     if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
     (void)hipFree(d);
     if (e != hipSuccess) return hip_fail(e, "p265r_batch_digest");
+    return p265r_batch_status(ctx, b);
+}
+
+int p265r_batch_digest_async(p265r_ctx* ctx, p265r_batch* b, int which, int slot) {
+    if (!ctx || !b || (which != 0 && which != 1) || slot < 0 || slot >= P265R_DIGEST_SLOTS) return P265R_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = join_sao(b)) return rc;
+    const size_t per_slot = sizeof(uint64_t) * 3 * (size_t)b->n_pics;
+    if (!b->d_dig) {
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&b->d_dig), per_slot * P265R_DIGEST_SLOTS));
+        HIP_TRY(hipMemsetAsync(b->d_dig, 0, per_slot * P265R_DIGEST_SLOTS, b->stream));
+    }
+    unsigned long long* d = b->d_dig + 3 * (size_t)b->n_pics * slot;
+    HIP_TRY(hipMemsetAsync(d, 0, per_slot, b->stream));
+    const dim3 grid((unsigned)((ctx->geo.h + kDigestRows - 1) / kDigestRows), 3, (unsigned)b->n_pics);
+    digest_kernel<<<grid, 256, 0, b->stream>>>(b->d_pics, ctx->geo, which == 0 ? 1 : 0, d);
+    HIP_TRY(hipGetLastError());
+    ctx->lane_busy |= 1u << b->lane;
+    return P265R_OK;
+}
+
+int p265r_batch_digest_slots(p265r_ctx* ctx, p265r_batch* b, uint64_t* out, int n_slots) {
+    if (!ctx || !b || !out || n_slots < 1 || n_slots > P265R_DIGEST_SLOTS) return P265R_EINVAL;
+    if (!b->d_dig) return P265R_ESTATE;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = join_sao(b)) return rc;
+    HIP_TRY(hipMemcpyAsync(out, b->d_dig, sizeof(uint64_t) * 3 * (size_t)b->n_pics * n_slots, hipMemcpyDeviceToHost,
+                           b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
     return p265r_batch_status(ctx, b);
 }
 
@@ -1322,6 +1360,7 @@ int p265r_batch_free(p265r_ctx* ctx, p265r_batch* b) {
     hipError_t e = b->stream ? hipStreamSynchronize(b->stream) : hipSuccess;
     if (b->intra_done) (void)hipEventDestroy(b->intra_done);
     if (b->sao_done) (void)hipEventDestroy(b->sao_done);
+    if (b->d_dig) (void)hipFree(b->d_dig);
     if (b->mem) {
         // keep the larger of (cache, this allocation) for the next upload (its runs are complete)
         if (!ctx->cache_mem || b->bytes > ctx->cache_bytes) {
@@ -1398,7 +1437,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
         "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"xg\": %d, \"last_launch_xg\": %d, "
-        "\"phase_order\": %d, "
+        "\"phase_order\": %d, \"row_launches\": {\"w12\": %lld, \"w8\": %lld, \"w16_split\": %lld, \"xg\": %lld, \"other\": %lld}, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : (P265R_PHASE_ORDER
@@ -1419,6 +1458,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         0,
 #endif
         P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, ctx->xg, ctx->last_xg ? 1 : 0, P265R_PHASE_ORDER,
+        ctx->row_launches[0], ctx->row_launches[1], ctx->row_launches[2], ctx->row_launches[3], ctx->row_launches[4],
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;
     if (size > 0) {
@@ -1427,6 +1467,12 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         buf[k] = 0;
     }
     return n;
+}
+
+int p265r_set_row_waves(p265r_ctx* ctx, int waves) {
+    if (!ctx || (waves != 0 && waves != 8 && waves != 12)) return P265R_EINVAL;
+    ctx->row_waves = waves;
+    return P265R_OK;
 }
 
 int p265r_set_timing(p265r_ctx* ctx, int enable) {

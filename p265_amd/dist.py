@@ -78,6 +78,26 @@ def finalize():
         _group = None
 
 
+def allgather_json(obj):
+    """Every rank's JSON-able ``obj`` -> the list over ranks (control plane), on every rank."""
+    import json
+    g = _group
+    if g is None or g.world == 1:
+        return [obj]
+    return [json.loads(p.decode()) for p in g.ctrl.allgather(json.dumps(obj).encode())]
+
+
+def rccl_ranks():
+    """ncclCommCount of every rank's communicator (the ranks RCCL itself sees), gathered over the control
+    plane; None when the group has no RCCL communicator (CPU, --no-rccl)."""
+    g = _group
+    if g is None:
+        return None
+    mine = g.nccl.count() if g.nccl is not None else None
+    got = allgather_json(mine)
+    return None if all(c is None for c in got) else got
+
+
 def broadcast_params(params, src=0):
     """Broadcast the params POD (records.PARAMS_DTYPE) from ``src`` to every rank:
     ncclBroadcast of its 32 bytes on a hipMalloc'd buffer, or over the control plane."""

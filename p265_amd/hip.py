@@ -54,6 +54,8 @@ def lib():
             "hipEventRecord": [vp, vp],
             "hipEventSynchronize": [vp],
             "hipEventElapsedTime": [ctypes.POINTER(ctypes.c_float), vp, vp],
+            "hipHostMalloc": [ctypes.POINTER(vp), sz, ctypes.c_uint],
+            "hipHostFree": [vp],
         }
         for name, args in sig.items():
             fn = getattr(h, name)
@@ -157,3 +159,38 @@ def copy_bandwidth_gbs(device, nbytes=4 << 30, reps=10):
         st.destroy()
         a.free()
         b.free()
+
+
+def pinned_copy_gbs(device, nbytes=1 << 30, reps=5):
+    """Host <-> device copy rates from pinned host memory (hipHostMalloc + hipMemcpyAsync, HIP events):
+    the PCIe ceiling of the back-end's uploads and downloads.  GB/s per direction."""
+    h = lib()
+    set_device(device)
+    host = ctypes.c_void_p()
+    check(h.hipHostMalloc(ctypes.byref(host), nbytes, 0), "hipHostMalloc")
+    dev = DeviceBuffer(nbytes)
+    st = Stream()
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    check(h.hipEventCreate(ctypes.byref(e0)), "hipEventCreate")
+    check(h.hipEventCreate(ctypes.byref(e1)), "hipEventCreate")
+    out = {}
+    try:
+        ctypes.memset(host, 1, nbytes)
+        for name, dst, src, kind in (("h2d_gbs", dev.ptr, host, H2D), ("d2h_gbs", host, dev.ptr, D2H)):
+            check(h.hipMemcpyAsync(dst, src, nbytes, kind, st.handle), "hipMemcpyAsync")
+            st.synchronize()
+            check(h.hipEventRecord(e0, st.handle), "hipEventRecord")
+            for _ in range(reps):
+                check(h.hipMemcpyAsync(dst, src, nbytes, kind, st.handle), "hipMemcpyAsync")
+            check(h.hipEventRecord(e1, st.handle), "hipEventRecord")
+            check(h.hipEventSynchronize(e1), "hipEventSynchronize")
+            ms = ctypes.c_float()
+            check(h.hipEventElapsedTime(ctypes.byref(ms), e0, e1), "hipEventElapsedTime")
+            out[name] = round(nbytes * reps / (ms.value * 1e-3) / 1e9, 2)
+        return out
+    finally:
+        h.hipEventDestroy(e0)
+        h.hipEventDestroy(e1)
+        st.destroy()
+        dev.free()
+        h.hipHostFree(host)

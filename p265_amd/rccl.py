@@ -91,6 +91,12 @@ class Rccl:
         check(h.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank), "ncclCommInitRank")
         self.stream = hip.Stream()
 
+    def count(self):
+        """ncclCommCount: the number of ranks in this communicator, as RCCL reports it."""
+        n = ctypes.c_int(0)
+        check(lib().ncclCommCount(self.comm, ctypes.byref(n)), "ncclCommCount")
+        return n.value
+
     def broadcast(self, data: bytes, root=0, nbytes=None) -> bytes:
         """ncclBroadcast of a byte string from ``root`` (others pass b"" and ``nbytes``)."""
         n = len(data) if self.rank == root else int(nbytes)

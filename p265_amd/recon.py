@@ -191,6 +191,22 @@ class ReconContext:
                    "p265r_batch_digest")
         return out.reshape(n, 3)
 
+    def digest_async(self, batch, slot, recon=False):
+        """Enqueue the device digest of the batch's planes after every run enqueued so far into digest
+        slot ``slot`` (0 .. _lib.DIGEST_SLOTS - 1) and return at once (p265r_batch_digest_async)."""
+        _lib.check(self.lib.p265r_batch_digest_async(self.handle, batch.handle, 1 if recon else 0, int(slot)),
+                   "p265r_batch_digest_async")
+
+    def digest_slots(self, batch, n_slots):
+        """Wait for the batch's lane; -> uint64 array [n_slots, n_pictures, 3] of the digest slots
+        (p265r_batch_digest_slots).  Raises P265RError like status()."""
+        n = len(batch.pics)
+        out = np.zeros(3 * n * n_slots, np.uint64)
+        _lib.check(self.lib.p265r_batch_digest_slots(self.handle, batch.handle,
+                                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), int(n_slots)),
+                   "p265r_batch_digest_slots")
+        return out.reshape(n_slots, n, 3)
+
     def job_count(self, batch):
         """(luma, chroma) intra jobs of the batch's last run (p265r_batch_job_count)."""
         lu, ch = ctypes.c_uint64(0), ctypes.c_uint64(0)
@@ -204,6 +220,10 @@ class ReconContext:
     def set_pipeline(self, depth):
         """Bind batches uploaded from now on round-robin to `depth` streams (p265r_set_pipeline)."""
         _lib.check(self.lib.p265r_set_pipeline(self.handle, int(depth)), "p265r_set_pipeline")
+
+    def set_row_waves(self, waves):
+        """Force the row kernel's build (8 / 12 waves per workgroup) or 0 = by run (p265r_set_row_waves)."""
+        _lib.check(self.lib.p265r_set_row_waves(self.handle, int(waves)), "p265r_set_row_waves")
 
     def set_timing(self, on=True):
         _lib.check(self.lib.p265r_set_timing(self.handle, int(bool(on))), "p265r_set_timing")

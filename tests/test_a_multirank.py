@@ -122,7 +122,7 @@ def test_bench_two_ranks_on_one_device():
     elapsed = d["ms_per_step"] * steps * 1e-3
     assert abs(d["value"] - 2 * 512 * 510 * steps / elapsed) <= 2e-3 * d["value"]
     assert d["verified"]["ok"] and d["verified"]["ranks_failed"] == 0 and d["verified"]["pictures"] > 0
-    assert "control plane" in d["collectives"]
+    assert "control plane" in d["collectives"]["kind"] and d["collectives"]["rccl_ranks"] is None
 
 
 def test_rccl_world1_broadcast_of_the_params():
@@ -139,3 +139,55 @@ def test_rccl_world1_broadcast_of_the_params():
         assert comm.exchange({0: b"x"}, {0: 1}) == {0: b"x"}      # and the next exchange still pairs
     finally:
         comm.close()
+
+
+def _child(args, env_extra, timeout=240):
+    env = {k: v for k, v in os.environ.items() if not k.startswith("P265R_")}
+    env.update(env_extra)
+    p = subprocess.run([sys.executable, "-u"] + args, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_self_launched_two_ranks():
+    """bench.py --gpus 2 with NO launcher (WORLD_SIZE unset): the parent starts the two rank processes itself
+    (--device-map 0,0: both on device 0, so --no-rccl) before anything touches the GPU, and exactly one line
+    comes back with n_gpus 2, both ranks' checks ok and the whole-job value."""
+    steps = 3
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("P265R_")}
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device-map", "0,0",
+                        "--no-rccl", "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-e2e", "--no-pcie"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == steps and d["config"]["pictures_per_gpu"] == 512
+    elapsed = d["ms_per_step"] * steps * 1e-3
+    assert abs(d["value"] - 2 * 512 * 510 * steps / elapsed) <= 2e-3 * d["value"]
+    assert d["verified"]["ok"] and d["verified"]["ranks_failed"] == 0 and d["verified"]["every_run"]["runs_checked"] == steps
+    assert d["collectives"]["devices"] == [0, 0] and d["collectives"]["rccl_ranks"] is None
+
+
+def test_xg_batches_side_by_side_on_sixteen_queues():
+    """Advisor (round 5): 16 small cross-group batches on 16 lanes with 16 hardware queues -- more cross-group
+    workgroups than the GPU holds at once, so chains are only partly resident; rows are claimed from a per-
+    chain ticket by running waves, so every run completes and equals the oracle (digest after every run)."""
+    p, res = _child([os.path.join(ROOT, "tests", "xg_worker.py"), "lanes"], {"GPU_MAX_HW_QUEUES": "16"})
+    assert p.returncode == 0 and res and res["ok"], (p.stdout + p.stderr)[-3000:]
+
+
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_broken_half_ctu_publish_fails_the_check_instance(variant):
+    """A P265R_BR_BROKEN build (prep publishes the bottom line's left half one job early) run with
+    P265R_TR_CHECK=1 on sanity.bin's frame 0 in component-major TB order: caught on every one of three runs --
+    by prep's extent check (variant 1: the batch reports P265R_EHIP) or, with that check compiled out
+    (variant 2), by the row kernel's poisoned half line (parity mismatch) -- never by timing."""
+    lib = os.path.join(ROOT, "p265_amd", "libp265r_brbroken%s.so" % variant)
+    assert os.path.exists(lib), "build the check variants first (make)"
+    p, res = _child([os.path.join(ROOT, "tests", "xg_worker.py"), "broken"], {"P265R_LIB": lib, "P265R_TR_CHECK": "1"})
+    assert p.returncode == 0 and res, (p.stdout + p.stderr)[-3000:]
+    want = "error" if variant == "1" else "mismatch"
+    assert all(o.startswith(want) for o in res["outcomes"]), res

@@ -92,3 +92,77 @@ def test_c5_batches_carry_consecutive_steps():
     a.c5_batch_units = 0                              # latency regime: one step per batch
     groups, _, cfg = b.build_workload(a, 0, 1)
     assert cfg["steps_per_batch"] == 1 and len(groups[0][1]) == 8
+
+
+def test_c5_one_k_for_every_rank():
+    """Units that do not divide over the ranks (8 over 3: 3, 3, 2): every rank's batch carries its units of
+    the SAME K steps (ceil(512 / 3) = 171), so the counted work (all units x K per run) is what the ranks
+    decode; build_workload takes K from this function for every rank."""
+    b = _bench()
+    assert b.c5_steps_per_batch(512, 8, 3) == 171
+    assert b.c5_steps_per_batch(512, 8, 1) == 64 and b.c5_steps_per_batch(512, 8, 8) == 512
+    assert b.c5_steps_per_batch(0, 8, 3) == 1
+
+
+def _run_bench(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("P265R_")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    r = _run_bench(["--gpus", "2", "--no-cpu-baseline"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr and not r.stdout.strip()
+    r = _run_bench(["--gpus", "1", "--no-cpu-baseline"], {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "--gpus 1" in r.stderr
+
+
+def test_bench_refuses_more_ranks_than_devices_and_bad_device_maps():
+    """--gpus N without a launcher spawns N ranks only when the devices exist (here: none visible), and never
+    prints a line claiming fewer GPUs; a device map must name one device per rank, and ranks sharing a
+    device must run without RCCL."""
+    r = _run_bench(["--gpus", "8", "--no-cpu-baseline"])
+    assert r.returncode == 2 and "needs 8 HIP device" in r.stderr and '"n_gpus"' not in r.stdout
+    r = _run_bench(["--gpus", "2", "--device-map", "0"])
+    assert r.returncode == 2 and "one device" in r.stderr
+    r = _run_bench(["--gpus", "2", "--device-map", "0,x"])
+    assert r.returncode == 2 and "comma-separated" in r.stderr
+    r = _run_bench(["--gpus", "2", "--device-map", "0,0"])
+    assert r.returncode == 2 and "--no-rccl" in r.stderr
+    r = _run_bench(["--gpus", "2", "--device-map", "0,0", "--no-rccl"])
+    assert r.returncode == 2 and "needs 1 HIP device" in r.stderr
+
+
+def test_launch_ranks_sets_the_launcher_environment(monkeypatch):
+    """The self-launch starts N children of bench.py with the environment torch.distributed.run gives its
+    ranks and returns the worst exit code (children stubbed: no GPU here)."""
+    import subprocess
+    import types
+    b = _bench()
+    seen = []
+
+    class FakeProc:
+        def __init__(self, cmd, env, cwd):
+            seen.append((cmd, env))
+            self.returncode = 3 if env["RANK"] == "1" else 0
+
+        def poll(self):
+            return self.returncode
+
+        def wait(self):
+            return self.returncode
+
+        def kill(self):
+            pass
+
+    monkeypatch.setattr(subprocess, "Popen", FakeProc)
+    monkeypatch.setattr(b, "visible_devices", lambda: 4)
+    a = types.SimpleNamespace(gpus=4, device_map=None, no_rccl=False)
+    rc = b.launch_ranks(a, ["--gpus", "4", "--steps", "3"])
+    assert rc == 3
+    assert [e["RANK"] for _, e in seen] == ["0", "1", "2", "3"] == [e["LOCAL_RANK"] for _, e in seen]
+    assert {e["WORLD_SIZE"] for _, e in seen} == {"4"} and {e["MASTER_ADDR"] for _, e in seen} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for _, e in seen}) == 1 and seen[0][0][-4:] == ["--gpus", "4", "--steps", "3"]

@@ -508,7 +508,20 @@ def _component_major(pic):
     return R.Picture(ctus=pic.ctus, tbs=tbs, coef=pic.coef, nofilter=pic.nofilter, meta=dict(pic.meta))
 
 
-def test_component_major_tb_order(recon_mod):
+@pytest.fixture(params=["auto", "xgchk", "xg8chk", "w16"])
+def xg_variant(request, monkeypatch):
+    """The latency layouts small batches run: cross-group chains (default xg 4), their checking instance
+    (P265R_TR_CHECK=1: top-right part of the row-above copy poisoned until its wait, the left half of every
+    bottom line served by the half-CTU publish alone, prep's `br` checked against the TB extents), xg 8
+    checked, and the one-workgroup-per-chain W = 16 split."""
+    env = {"auto": {}, "xgchk": {"P265R_TR_CHECK": "1"}, "xg8chk": {"P265R_XG": "8", "P265R_TR_CHECK": "1"},
+           "w16": {"P265R_XG": "0"}}[request.param]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_component_major_tb_order(recon_mod, xg_variant):
     params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5)
     pics = [_component_major(synth.make_picture(params, 4040 + s, perf=False)) for s in range(2)]
     _check(recon_mod, params, pics, "component-major")
