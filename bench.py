@@ -184,6 +184,9 @@ def parse(argv=None):
                     help="N > 1: comma-separated HIP device of each local rank (default: local rank i on device i); "
                          "ranks sharing a device need --no-rccl (tests: --gpus 2 --device-map 0,0 --no-rccl)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive back-end leg")
+    ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 9, 10),
+                    help="c3: BitDepth of the synthetic pictures (9 / 10: the Main 10 path -- uint16 planes, per-diagonal "
+                         "intra kernel, loopfilter16.h; not the headline)")
     return ap.parse_args(argv)
 
 
@@ -218,7 +221,7 @@ def host_info():
     return {"cpu_model": model, "host_cores_total": total, "cpu_share": share}
 
 
-def algorithmic_bytes(pics):
+def algorithmic_bytes(pics, pel_bytes=1):
     """B = 2C + 16 N_TB + 16 N_CU + 3 S + 32 N_CTU per picture.
 
     N_CU is not carried by the records (each TB record holds the CU-level fields the path
@@ -230,7 +233,7 @@ def algorithmic_bytes(pics):
     for p in pics:
         c = p.n_coded_coef
         ntb, nctu = len(p.tbs), len(p.ctus)
-        s = p.meta["samples"]
+        s = p.meta["samples"] * pel_bytes                  # output bytes (2 per sample above 8 bits)
         tot += 2 * c + 16 * ntb + 3 * s + 32 * nctu
         intra += 2 * c + 16 * ntb + s + 32 * nctu
         resid += 4 * c + 8 * int(((p.tbs["flags"] & 1) != 0).sum())
@@ -456,7 +459,7 @@ def pcie_leg(params, pics, device, steps=3):
     # coefficients + TB / CTU records + the 8-B residual job of every coded TB (p265r_batch_upload's H2D copies)
     h2d_bytes = sum(2 * p.n_coded_coef + R.TB_DTYPE.itemsize * len(p.tbs) + R.CTU_DTYPE.itemsize * len(p.ctus) +
                     8 * int(((p.tbs["flags"] & R.TB_CBF) != 0).sum()) for p in pics)
-    d2h_bytes = sum(p.meta["samples"] for p in pics)
+    d2h_bytes = sum(p.meta["samples"] for p in pics) * (1 if int(params["bit_depth_luma"]) == 8 else 2)
     nnz = sum(int(np.count_nonzero(p.coef)) for p in {id(p): p for p in pics}.values())
     coded = sum(p.n_coded_coef for p in {id(p): p for p in pics}.values())
     out = {"pictures_per_step": len(pics), "steps": steps}
@@ -516,15 +519,17 @@ def build_workload(a, rank, world):
     from p265_amd import dist, synth, tiles
     from p265_amd import records as R
     if a.workload == "c3":
-        params = R.make_params(pic_width=1920, pic_height=1080)
+        params = R.make_params(pic_width=1920, pic_height=1080, bit_depth_luma=a.bit_depth, bit_depth_chroma=a.bit_depth)
         params = dist.broadcast_params(params)                  # RCCL broadcast of the SPS/PPS POD
         uniq = [synth.make_picture(params, 268 + 1000 * rank + i, perf=True, deblocking=a.deblocking)
                 for i in range(a.unique)]
         for p in uniq:
             p.meta["samples"] = 1920 * 1080 * 3 // 2
         pics = [uniq[i % a.unique] for i in range(a.frames)]
-        cfg = {"workload": "C3/C4: 1080p all-intra + %sSAO, %d pictures per GPU per step (%d distinct)"
-                           % ("deblocking + " if a.deblocking else "", a.frames, a.unique),
+        cfg = {"workload": "C3/C4: 1080p all-intra + %sSAO, %d pictures per GPU per step (%d distinct)%s"
+                           % ("deblocking + " if a.deblocking else "", a.frames, a.unique,
+                              "" if a.bit_depth == 8 else ", BitDepth %d (Main 10 path, not the headline)" % a.bit_depth),
+               "bit_depth": a.bit_depth,
                "pictures_per_gpu": a.frames, "ctus_per_picture": len(pics[0].ctus), "ctb": 64,
                "parallelism": "picture-sharded x%d (picture f -> rank f mod N)" % world}
         return [(params, pics)], (params, uniq, "1080p pictures"), cfg
@@ -720,7 +725,7 @@ def main(argv=None):
     host = host_info()
     # pure-Python CPU baseline first, in a child process, before this process touches the GPU
     py_base = None
-    if world_env == 1 and not a.no_cpu_baseline and a.workload == "c3":
+    if world_env == 1 and not a.no_cpu_baseline and a.workload == "c3" and a.bit_depth == 8:
         py_base = cpu_baseline_python(host["cpu_share"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if local_rank >= len(dmap):
@@ -811,7 +816,7 @@ def main(argv=None):
     else:                                  # every tile unit of the batch's steps, over all ranks
         total_ctus = cfg["ctus_all_units"] * cfg["steps_per_batch"] * a.steps
     value = total_ctus / elapsed
-    tot_b, intra_b, res_b, sao_b = algorithmic_bytes(pics)
+    tot_b, intra_b, res_b, sao_b = algorithmic_bytes(pics, 1 if a.bit_depth == 8 else 2)
     launches_per_step = acc["intra_launches"] / a.steps
     avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     bytes_per_launch = intra_b / launches_per_step
@@ -823,10 +828,11 @@ def main(argv=None):
         "value": round(value, 1), "unit": "CTU/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak" if a.workload == "c3" else "strong",
-        "vs_baseline": None, "dtype": "u8 samples / int16 coefficients (integer)",
+        "vs_baseline": None, "dtype": "%s samples / int16 coefficients (integer)" % ("u8" if a.bit_depth == 8 else "u16"),
         "data": "synthetic: seeded all-intra records with sanity.bin statistics (p265_amd/synth.py)",
         "config": cfg,
-        "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel", "achieved": round(achieved, 2),
+        "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel" if a.bit_depth == 8 else
+                     "intra_step_kernel<uint16_t> (one launch per anti-diagonal)", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
                                         % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
@@ -896,7 +902,7 @@ def main(argv=None):
         ctx.close()
     if rank == 0 and world == 1 and not a.no_pcie and a.workload == "c3":
         out["pcie"] = pcie_leg(groups[0][0], groups[0][1], local)
-    if rank == 0 and world == 1 and not a.no_e2e and a.workload == "c3":
+    if rank == 0 and world == 1 and not a.no_e2e and a.workload == "c3" and a.bit_depth == 8:
         out["end_to_end"] = end_to_end(local, threads=min(16, host["cpu_share"]))
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -63,8 +63,9 @@ def _decode(params, pics, threads, with_recon):
             nf = np.ascontiguousarray(p.nofilter, np.uint8)
             keep.append(nf)
             a.nofilter = nf.ctypes.data
-        rec = [np.zeros(s, np.uint8) for s in shapes]
-        out = [np.zeros(s, np.uint8) for s in shapes]
+        dts = R.plane_dtypes(params)
+        rec = [np.zeros(s, dt) for s, dt in zip(shapes, dts)]
+        out = [np.zeros(s, dt) for s, dt in zip(shapes, dts)]
         for k in range(3):
             a.out[k] = out[k].ctypes.data
             if with_recon:

@@ -185,13 +185,17 @@ static void predict(const int* p, int n, int mode, int c, int bd, int* pred) {
 #undef TOP
 }
 
-static void recon_tb(const geo_t* g, const p265r_params* prm, uint8_t* planes[3], const int stride[3],
+/* Sample planes are uint16_t inside the oracle whatever the bit depth (8..12); the caller's planes are
+ * uint8_t for BitDepth 8 and uint16_t (little-endian) above (p265r_picture). */
+typedef uint16_t pel;
+
+static void recon_tb(const geo_t* g, const p265r_params* prm, pel* planes[3], const int stride[3],
                      const p265r_tb* t, const int16_t* coef) {
     const int c = t->c_idx, log2 = t->log2_size, n = 1 << log2, sub = c ? 1 : 0;
     const int bd = c ? prm->bit_depth_chroma : prm->bit_depth_luma;
     const int maxv = (1 << bd) - 1;
     const int x0 = t->x, y0 = t->y;
-    uint8_t* pl = planes[c];
+    pel* pl = planes[c];
     const int st = stride[c];
     int res[1024], pred[1024];
     if (t->flags & (P265R_TB_CBF | P265R_TB_PCM)) residual(coef + t->coef_off, log2, c, t->qp, t->flags, bd, res);
@@ -244,12 +248,12 @@ static void recon_tb(const geo_t* g, const p265r_params* prm, uint8_t* planes[3]
         predict(p, n, t->pred_mode, c, bd, pred);
     }
     for (int y = 0; y < n; ++y)
-        for (int x = 0; x < n; ++x) pl[(y0 + y) * st + x0 + x] = (uint8_t)clip3(0, maxv, (long long)pred[y * n + x] + res[y * n + x]);
+        for (int x = 0; x < n; ++x) pl[(y0 + y) * st + x0 + x] = (pel)clip3(0, maxv, (long long)pred[y * n + x] + res[y * n + x]);
 }
 
 static inline int sgn(int v) { return (v > 0) - (v < 0); }
 
-static void sao(const geo_t* g, const p265r_params* prm, const p265r_picture* pic, uint8_t* rec[3], uint8_t* out[3],
+static void sao(const geo_t* g, const p265r_params* prm, const p265r_picture* pic, pel* rec[3], pel* out[3],
                 const int stride[3]) {
     const int nfw = (g->w + 7) / 8;
     for (int rs = 0; rs < g->wc * g->hc; ++rs) {
@@ -304,7 +308,7 @@ static void sao(const geo_t* g, const p265r_params* prm, const p265r_picture* pi
                             r = clip3(0, maxv, v + off[e]);
                         }
                     }
-                    out[c][y * stride[c] + x] = (uint8_t)r;
+                    out[c][y * stride[c] + x] = (pel)r;
                 }
         }
     }
@@ -329,7 +333,8 @@ typedef struct {
     const uint8_t* nofilter;
     int nfw, w4;
     uint32_t* org;   /* per 4x4 luma unit: origin (x | y << 16) of the luma TB covering it */
-    uint8_t* qpy;    /* per 4x4 luma unit: QpY                                           */
+    int16_t* qpy;    /* per 4x4 luma unit: QpY (negative down to -QpBdOffsetY above 8 bits)  */
+    int bdl, bdc;    /* BitDepthY, BitDepthC                                             */
 } dbk_t;
 
 /* bS == 2 && filterEdgeFlag for the edge between luma samples p0 (xp,yp) and q0 (xq,yq) */
@@ -349,12 +354,13 @@ static inline int dbk_nf(const dbk_t* d, int x, int y) { return d->nofilter && d
 static inline int dbk_qp(const dbk_t* d, int x, int y) { return d->qpy[(y >> 2) * d->w4 + (x >> 2)]; }
 
 /* s[i*step_i + k*step_k]: sample at distance i from the edge (i < 0: P side, p_i = s[-(i+1)]) on line k */
-static void dbk_luma_seg(uint8_t* s, int step_i, int step_k, int qpp, int qpq, int boff, int toff, int nop, int noq) {
+static void dbk_luma_seg(pel* s, int step_i, int step_k, int qpp, int qpq, int boff, int toff, int nop, int noq, int bd) {
 #define PS(i, k) s[-((i) + 1) * step_i + (k) * step_k]
 #define QS(i, k) s[(i) * step_i + (k) * step_k]
     const int qpl = (qpq + qpp + 1) >> 1;
-    const int beta = BETA_T[clip3(0, 51, qpl + 2 * boff)];
-    const int tc = TC_T[clip3(0, 53, qpl + 2 + 2 * toff)];
+    const int beta = BETA_T[clip3(0, 51, qpl + 2 * boff)] * (1 << (bd - 8));      /* 8.7.2.5.3: beta' and tC' scaled */
+    const int tc = TC_T[clip3(0, 53, qpl + 2 + 2 * toff)] * (1 << (bd - 8));
+    const int maxv = (1 << bd) - 1;
     const int dp0 = abs(PS(2, 0) - 2 * PS(1, 0) + PS(0, 0)), dp3 = abs(PS(2, 3) - 2 * PS(1, 3) + PS(0, 3));
     const int dq0 = abs(QS(2, 0) - 2 * QS(1, 0) + QS(0, 0)), dq3 = abs(QS(2, 3) - 2 * QS(1, 3) + QS(0, 3));
     if (dp0 + dq0 + dp3 + dq3 >= beta) return;
@@ -372,26 +378,26 @@ static void dbk_luma_seg(uint8_t* s, int step_i, int step_k, int qpp, int qpq, i
         const int q0 = QS(0, k), q1 = QS(1, k), q2 = QS(2, k), q3 = QS(3, k);
         if (strong) {
             if (!nop) {
-                PS(0, k) = (uint8_t)clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-                PS(1, k) = (uint8_t)clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2);
-                PS(2, k) = (uint8_t)clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+                PS(0, k) = (pel)clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+                PS(1, k) = (pel)clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2);
+                PS(2, k) = (pel)clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
             }
             if (!noq) {
-                QS(0, k) = (uint8_t)clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-                QS(1, k) = (uint8_t)clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2);
-                QS(2, k) = (uint8_t)clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3);
+                QS(0, k) = (pel)clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+                QS(1, k) = (pel)clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2);
+                QS(2, k) = (pel)clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3);
             }
         } else {
             int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
             if (abs(delta) >= tc * 10) continue;
             delta = clip3(-tc, tc, delta);
             if (!nop) {
-                PS(0, k) = (uint8_t)clip3(0, 255, p0 + delta);
-                if (dep) PS(1, k) = (uint8_t)clip3(0, 255, p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1));
+                PS(0, k) = (pel)clip3(0, maxv, p0 + delta);
+                if (dep) PS(1, k) = (pel)clip3(0, maxv, p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1));
             }
             if (!noq) {
-                QS(0, k) = (uint8_t)clip3(0, 255, q0 - delta);
-                if (deq) QS(1, k) = (uint8_t)clip3(0, 255, q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1));
+                QS(0, k) = (pel)clip3(0, maxv, q0 - delta);
+                if (deq) QS(1, k) = (pel)clip3(0, maxv, q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1));
             }
         }
     }
@@ -399,15 +405,16 @@ static void dbk_luma_seg(uint8_t* s, int step_i, int step_k, int qpp, int qpq, i
 #undef QS
 }
 
-static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture* pic, uint8_t* pl[3], const int stride[3]) {
+static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture* pic, pel* pl[3], const int stride[3]) {
     int any = 0;
     for (int i = 0; i < g->wc * g->hc; ++i) any |= g->ctus[i].flags & P265R_CTU_DEBLOCK;
     if (!any) return;
     dbk_t d;
     d.g = g; d.prm = prm; d.nofilter = pic->nofilter; d.nfw = (g->w + 7) / 8; d.w4 = g->w >> 2;
+    d.bdl = prm->bit_depth_luma; d.bdc = prm->bit_depth_chroma;
     const int h4 = g->h >> 2;
     d.org = (uint32_t*)calloc((size_t)d.w4 * h4, sizeof(uint32_t));
-    d.qpy = (uint8_t*)calloc((size_t)d.w4 * h4, 1);
+    d.qpy = (int16_t*)calloc((size_t)d.w4 * h4, sizeof(int16_t));
     for (uint32_t t = 0; t < pic->n_tbs; ++t) {
         const p265r_tb* tb = &pic->tbs[t];
         if (tb->c_idx) continue;
@@ -416,7 +423,7 @@ static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture
             for (int i = 0; i < n4; ++i) {
                 const size_t u = (size_t)((tb->y >> 2) + j) * d.w4 + (tb->x >> 2) + i;
                 d.org[u] = (uint32_t)tb->x | (uint32_t)tb->y << 16;
-                d.qpy[u] = tb->qp;   /* 8-bit: QpBdOffsetY = 0 */
+                d.qpy[u] = (int16_t)(tb->qp - 6 * (d.bdl - 8));   /* QpY = Qp'Y - QpBdOffsetY */
             }
     }
     for (int dir = 0; dir < 2; ++dir) {          /* 0: vertical edges, 1: horizontal edges */
@@ -427,9 +434,9 @@ static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture
                 const int xq = dir ? s0 : e, yq = dir ? e : s0, xp = dir ? xq : xq - 1, yp = dir ? yq - 1 : yq;
                 if (!dbk_edge(&d, xp, yp, xq, yq)) continue;
                 const uint8_t off = g->ctus[ctb_of(g, xq, yq)].deblock_offsets;
-                uint8_t* s = pl[0] + (size_t)yq * stride[0] + xq;
+                pel* s = pl[0] + (size_t)yq * stride[0] + xq;
                 dbk_luma_seg(s, dir ? stride[0] : 1, dir ? 1 : stride[0], dbk_qp(&d, xp, yp), dbk_qp(&d, xq, yq),
-                             nib(off & 15), nib(off >> 4), dbk_nf(&d, xp, yp), dbk_nf(&d, xq, yq));
+                             nib(off & 15), nib(off >> 4), dbk_nf(&d, xp, yp), dbk_nf(&d, xq, yq), d.bdl);
             }
         /* chroma */
         for (int c = 1; c < 3; ++c) {
@@ -443,15 +450,16 @@ static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture
                     if (!dbk_edge(&d, lxp, lyp, lxq, lyq)) continue;
                     const int toff = nib(g->ctus[ctb_of(g, lxq, lyq)].deblock_offsets >> 4);
                     const int qpc = qpc_of(((dbk_qp(&d, lxq, lyq) + dbk_qp(&d, lxp, lyp) + 1) >> 1) + cqp);
-                    const int tc = TC_T[clip3(0, 53, qpc + 2 + 2 * toff)];
+                    const int tc = TC_T[clip3(0, 53, qpc + 2 + 2 * toff)] * (1 << (d.bdc - 8));
+                    const int maxc = (1 << d.bdc) - 1;
                     const int nop = dbk_nf(&d, lxp, lyp), noq = dbk_nf(&d, lxq, lyq);
                     const int si = dir ? stride[c] : 1, sk = dir ? 1 : stride[c];
                     for (int k = 0; k < 4; ++k) {
-                        uint8_t* q = pl[c] + (size_t)yq * stride[c] + xq + k * sk;
+                        pel* q = pl[c] + (size_t)yq * stride[c] + xq + k * sk;
                         const int p0 = q[-si], p1 = q[-2 * si], q0 = q[0], q1 = q[si];
                         const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
-                        if (!nop) q[-si] = (uint8_t)clip3(0, 255, p0 + delta);
-                        if (!noq) q[0] = (uint8_t)clip3(0, 255, q0 - delta);
+                        if (!nop) q[-si] = (pel)clip3(0, maxc, p0 + delta);
+                        if (!noq) q[0] = (pel)clip3(0, maxc, q0 - delta);
                     }
                 }
         }
@@ -460,11 +468,19 @@ static void deblock(const geo_t* g, const p265r_params* prm, const p265r_picture
     free(d.qpy);
 }
 
+/* caller plane <-> oracle plane (uint8_t samples at BitDepth 8, uint16_t above) */
+static void plane_out(void* dst, const pel* src, size_t n, int bd) {
+    if (bd > 8) memcpy(dst, src, n * sizeof(pel));
+    else for (size_t i = 0; i < n; ++i) ((uint8_t*)dst)[i] = (uint8_t)src[i];
+}
+
 /* Decode n pictures: writes pics[i].recon[] (if set) and pics[i].out[] (if set).
  * Returns 0 or a negative P265R_* code.  n_threads <= 0: OpenMP default. */
 int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int n_threads) {
     if (!prm || !pics || n < 0) return P265R_EINVAL;
-    if (prm->bit_depth_luma != 8 || prm->bit_depth_chroma != 8 || prm->chroma_format_idc != 1) return P265R_EUNSUPPORTED;
+    if (prm->bit_depth_luma < 8 || prm->bit_depth_luma > 12 || prm->bit_depth_chroma < 8 || prm->bit_depth_chroma > 12 ||
+        prm->chroma_format_idc != 1)
+        return P265R_EUNSUPPORTED;
     init_dct();
     int err = 0;
 #ifdef _OPENMP
@@ -477,12 +493,12 @@ int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int
                        ((prm->pic_height + (1 << prm->ctb_log2_size) - 1) >> prm->ctb_log2_size);
         int* rs2ts = (int*)malloc(sizeof(int) * nc);
         const int stride[3] = {prm->pic_width, prm->pic_width / 2, prm->pic_width / 2};
-        uint8_t* rec[3];
-        uint8_t* out[3];
+        const int bd[3] = {prm->bit_depth_luma, prm->bit_depth_chroma, prm->bit_depth_chroma};
+        size_t sz[3];
+        pel* rec[3];
         for (int c = 0; c < 3; ++c) {
-            const size_t sz = (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height);
-            rec[c] = pics[i].recon[c] ? (uint8_t*)pics[i].recon[c] : (uint8_t*)malloc(sz);
-            out[c] = (uint8_t*)pics[i].out[c];
+            sz[c] = (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height);
+            rec[c] = (pel*)malloc(sz[c] * sizeof(pel));
         }
         geo_init(&g, prm, pics[i].ctus, rs2ts);
         /* CTUs in tile-scan order, TBs in record order */
@@ -493,22 +509,28 @@ int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int
             for (uint32_t k = cu->tb_begin; k < cu->tb_begin + cu->tb_count; ++k)
                 recon_tb(&g, prm, rec, stride, &pics[i].tbs[k], pics[i].coef);
         }
-        if (out[0] && out[1] && out[2]) {
+        for (int c = 0; c < 3; ++c)
+            if (pics[i].recon[c]) plane_out(pics[i].recon[c], rec[c], sz[c], bd[c]);
+        if (pics[i].out[0] && pics[i].out[1] && pics[i].out[2]) {
             /* in-loop filters: deblocking into a scratch copy (rec stays the filter input), then SAO */
-            uint8_t* dbk[3];
+            pel* dbk[3];
+            pel* out[3];
             for (int c = 0; c < 3; ++c) {
-                const size_t sz = (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height);
-                dbk[c] = (uint8_t*)malloc(sz);
-                memcpy(dbk[c], rec[c], sz);
+                dbk[c] = (pel*)malloc(sz[c] * sizeof(pel));
+                out[c] = (pel*)malloc(sz[c] * sizeof(pel));
+                memcpy(dbk[c], rec[c], sz[c] * sizeof(pel));
             }
             deblock(&g, prm, &pics[i], dbk, stride);
             if (prm->sample_adaptive_offset) sao(&g, prm, &pics[i], dbk, out, stride);
             else
-                for (int c = 0; c < 3; ++c)
-                    memcpy(out[c], dbk[c], (size_t)stride[c] * (c ? prm->pic_height / 2 : prm->pic_height));
-            for (int c = 0; c < 3; ++c) free(dbk[c]);
+                for (int c = 0; c < 3; ++c) memcpy(out[c], dbk[c], sz[c] * sizeof(pel));
+            for (int c = 0; c < 3; ++c) {
+                plane_out(pics[i].out[c], out[c], sz[c], bd[c]);
+                free(dbk[c]);
+                free(out[c]);
+            }
         }
-        for (int c = 0; c < 3; ++c) if (!pics[i].recon[c]) free(rec[c]);
+        for (int c = 0; c < 3; ++c) free(rec[c]);
         free(order);
         free(rs2ts);
     }

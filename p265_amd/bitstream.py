@@ -149,11 +149,28 @@ def _view(ptr, n, dtype, owner):
 
 
 def plane_hash(plane, hash_type):
-    """decoded_picture_hash value (D.3.19) of one uint8 plane, as the SEI carries it.
+    """decoded_picture_hash value (D.3.19) of one uint8 or uint16 plane, as the SEI carries it.
 
-    MD5 of an 8-bit plane is the MD5 of its samples in raster order (one byte each), which
-    hashlib computes without the GIL and faster than the library's portable MD5; CRC and
-    checksum (and the same MD5, for the tests) come from p265fe_plane_hash."""
+    MD5 and CRC run over pictureData: the samples in raster order, one byte each at BitDepth 8 and
+    two (little-endian) above (D.3.19), so a uint16 plane is hashed as its bytes (the CRC through
+    p265fe_plane_hash on a row of 2W bytes).  MD5 comes from hashlib (no GIL, faster than the
+    library's portable MD5).  The checksum sums per SAMPLE ((sample & 0xFF) ^ xorMask, plus
+    (sample >> 8) ^ xorMask above 8 bits, D-23): p265fe_plane_hash at 8 bits, numpy above."""
+    p = np.ascontiguousarray(plane)
+    if p.dtype == np.uint16:
+        p = p.astype("<u2", copy=False)
+        if int(hash_type) == HASH_MD5:
+            return hashlib.md5(memoryview(p).cast("B")).digest()
+        if int(hash_type) == HASH_CRC:
+            return plane_hash_native(p.view(np.uint8), hash_type)
+        if int(hash_type) == HASH_CHECKSUM:
+            h, w = p.shape
+            x, y = np.arange(w, dtype=np.uint64), np.arange(h, dtype=np.uint64)[:, None]
+            mask = (x & np.uint64(0xFF)) ^ (y & np.uint64(0xFF)) ^ (x >> np.uint64(8)) ^ (y >> np.uint64(8))
+            v = p.astype(np.uint64)
+            s = int((((v & np.uint64(0xFF)) ^ mask).sum() + ((v >> np.uint64(8)) ^ mask).sum())) & 0xFFFFFFFF
+            return s.to_bytes(4, "big")
+        raise ValueError("unknown hash type %r" % hash_type)
     p = np.ascontiguousarray(plane, np.uint8)
     if int(hash_type) == HASH_MD5:
         return hashlib.md5(memoryview(p).cast("B")).digest()

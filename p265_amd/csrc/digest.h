@@ -2,9 +2,9 @@
 // resident batch (bench.py) check EVERY picture it timed against the oracle without downloading
 // the planes.  No counterpart in the reference (its planes are never produced, cu.py:487-488).
 //
-// digest(plane) = sum over the plane's 4-sample words (row y, word i; W/4 words per row, the
-// picture's own width) of mix64(word | (y * W/4 + i) << 32) mod 2^64, mix64 = the splitmix64
-// finalizer.  Position-keyed and order-free, so the partial sums of any split of the plane add up;
+// digest(plane) = sum over the plane's 32-bit words (row y, word i; K words per row: W/4 of 4 samples
+// for uint8_t planes, W/2 of 2 samples for uint16_t planes (Geo::pel16); W the picture's own width) of
+// mix64(word | (y * K + i) << 32) mod 2^64, mix64 = the splitmix64 finalizer.  Position-keyed and order-free, so the partial sums of any split of the plane add up;
 // p265_amd/digest.py restates it with numpy for the host side.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -33,9 +33,9 @@ __global__ __launch_bounds__(256) void digest_kernel(const DevPic* __restrict__ 
     const int y0 = blockIdx.x * kDigestRows;
     if (y0 >= h) return;                                 // (block-uniform)
     const int rows = min(kDigestRows, h - y0);
-    const int wpr = w >> 2;                              // words per row (widths are multiples of 4)
+    const int wpr = g.pel16 ? w >> 1 : w >> 2;          // words per row (widths are multiples of 4)
     const uint8_t* plane = use_out ? P.out[c] : P.rec[c];
-    const int stride = g.stride[c];
+    const int stride = g.stride[c] << (g.pel16 ? 1 : 0);  // bytes
     uint64_t acc = 0;
     for (int e = threadIdx.x; e < rows * wpr; e += 256) {
         const int yy = e / wpr, i = e - yy * wpr;

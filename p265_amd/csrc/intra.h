@@ -20,6 +20,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "../../include/p265r.h"
 #include "tables.h"
 
@@ -87,6 +88,8 @@ struct Geo {                    // batch-uniform geometry
                                 // wait and serves the left half of every CTU's bottom line from the half-CTU
                                 // publish alone (checks prep's `tr` and `br` deterministically); the prep kernel
                                 // checks `br` against the TBs' extents (error word bit 1)
+    int pel16;                  // samples are uint16_t (BitDepth 9..10, Main 10): planes of stride[] samples of 2
+                                // bytes, the per-diagonal intra kernel and loopfilter16.h (else uint8_t)
 };
 
 // A/B: s_setprio of the bandwidth-phase kernels' waves (residual, prep, SAO), 0 = default
@@ -134,13 +137,14 @@ __device__ __forceinline__ bool ctu_same_region(const p265r_ctu& a, const p265r_
     return a.slice_addr == b.slice_addr && a.tile_id == b.tile_id;
 }
 
-struct CtuLds {
-    uint8_t  y[64 * 64];        // interior luma, stride 64
-    uint8_t  c[2][32 * 32];     // interior chroma, stride 32
-    uint8_t  ytop[132];         // row y=-1, x = -1 .. 127  (index x+1)
-    uint8_t  ctop[2][68];       // row y=-1, x = -1 .. 63
-    uint8_t  yleft[64];         // column x=-1, y = 0 .. 63
-    uint8_t  cleft[2][32];
+template <typename T>           // sample type: uint8_t (BitDepth 8) or uint16_t (BitDepth 9..10, Geo::pel16)
+struct CtuLdsT {
+    T        y[64 * 64];        // interior luma, stride 64
+    T        c[2][32 * 32];     // interior chroma, stride 32
+    T        ytop[132];         // row y=-1, x = -1 .. 127  (index x+1)
+    T        ctop[2][68];       // row y=-1, x = -1 .. 63
+    T        yleft[64];         // column x=-1, y = 0 .. 63
+    T        cleft[2][32];
     uint16_t ref[2][136];       // linear reference arrays (raw/substituted, filtered)
 };
 
@@ -252,11 +256,14 @@ __host__ __device__ __forceinline__ uint32_t ref_avail_mask32(int c, int xr, int
     return (bl ? m_bl : 0u) | (left ? m_l : 0u) | (corner ? m_c : 0u) | (top ? m_t : 0u) | (tr ? m_tr : 0u);
 }
 
+// One launch per anti-diagonal step (P265R_SCHEDULE=steps; the only schedule of the 16-bit sample path,
+// Main 10: T = uint16_t, planes of Geo::stride samples of 2 bytes).
+template <typename T>
 __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict__ pics,
                                                        const int16_t* __restrict__ pool,
                                                        const int16_t* __restrict__ resid,
                                                        Geo g, int step, int cy_min) {
-    __shared__ CtuLds L;
+    __shared__ CtuLdsT<T> L;
     const int lane = threadIdx.x;
     const int cy = cy_min + blockIdx.x;
     const int cx = step - 2 * cy;
@@ -283,10 +290,10 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
         const int cs = ctb >> sub;
         const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
         const int xb = x0 >> sub, yb = y0 >> sub;
-        const uint8_t* plane = P.rec[c];
+        const T* plane = reinterpret_cast<const T*>(P.rec[c]);
         const int st = (c ? g.stride[1] : g.stride[0]);
-        uint8_t* top = c ? L.ctop[c - 1] : L.ytop;
-        uint8_t* left = c ? L.cleft[c - 1] : L.yleft;
+        T* top = c ? L.ctop[c - 1] : L.ytop;
+        T* left = c ? L.cleft[c - 1] : L.yleft;
         for (int e = lane; e <= 2 * cs; e += 64) {
             const int x = e - 1;
             const unsigned need = x < 0 ? 4u : (x < cs ? 2u : 8u);
@@ -306,10 +313,10 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
         const int xr = tb.x - (x0 >> sub), yr = tb.y - (y0 >> sub);   // CTB-relative, component units
         const int bd = (c ? g.bd[1] : g.bd[0]);
         const int maxv = (1 << bd) - 1;
-        uint8_t* interior = c ? L.c[c - 1] : L.y;
+        T* interior = c ? L.c[c - 1] : L.y;
         const int ist = c ? 32 : 64;
-        uint8_t* top = c ? L.ctop[c - 1] : L.ytop;
-        uint8_t* left = c ? L.cleft[c - 1] : L.yleft;
+        T* top = c ? L.ctop[c - 1] : L.ytop;
+        T* left = c ? L.cleft[c - 1] : L.yleft;
 
         // samples owned by this lane: S consecutive in raster order of the TB
         const int nn = n * n;
@@ -491,8 +498,13 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
             }
         }
         // ---- reconstruction: Clip1(pred + res) into the CTU's LDS image ------------
-        if (own) {
-            uint8_t* dst = interior + (yr + sy) * ist + xr + sx;
+        if (own && sizeof(T) == 2) {
+            T* dst = interior + (yr + sy) * ist + xr + sx;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (i < S) dst[i] = (T)min(max(pred[i] + res[i], 0), maxv);
+        } else if (own) {
+            uint8_t* dst = reinterpret_cast<uint8_t*>(interior + (yr + sy) * ist + xr + sx);
             if (S == 16) {
                 uint32_t w[4];
 #pragma unroll
@@ -524,16 +536,17 @@ __global__ __launch_bounds__(64) void intra_step_kernel(const DevPic* __restrict
         const int W = c ? g.cw : g.w, H = c ? g.ch : g.h;
         const int xb = x0 >> sub, yb = y0 >> sub;
         const int wv = min(cs, W - xb), hv = min(cs, H - yb);
-        const uint8_t* src = c ? L.c[c - 1] : L.y;
+        const T* src = c ? L.c[c - 1] : L.y;
         const int ist = c ? 32 : 64;
-        uint8_t* plane = P.rec[c];
+        T* plane = reinterpret_cast<T*>(P.rec[c]);
         const int st = (c ? g.stride[1] : g.stride[0]);
-        // 4-byte granules (plane widths are multiples of 4: MinCbSize >= 8)
+        // 4-sample granules (plane widths are multiples of 4: MinCbSize >= 8): 4 or 8 bytes
+        typedef typename std::conditional<sizeof(T) == 1, uint32_t, uint2>::type G4;
         const int gpr = wv >> 2;
         for (int e = lane; e < gpr * hv; e += 64) {
             const int yy = e / gpr, xx = (e - yy * gpr) << 2;
-            *reinterpret_cast<uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
-                *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
+            *reinterpret_cast<G4*>(plane + (size_t)(yb + yy) * st + xb + xx) =
+                *reinterpret_cast<const G4*>(src + yy * ist + xx);
         }
     }
 }

@@ -168,4 +168,18 @@ int p265probe_stream(int device, double bytes, double* copy_gbs, double* read_gb
     return 0;
 }
 
+// which: 0 = the round-5 row-kernel mix (VALU 131, SALU 81, LDS 15 per job), 1 = its VALU alone,
+// 2 = its SALU alone, 3 = its LDS alone.  -> CU-cycles per job (s_memtime, the slowest wave) and the
+// launch time.  Returns 0, or < 0 on a HIP error.
+int p265probe_issue(int device, int which, int jobs, double* cycles_per_job_cu, double* ms) {
+    if (!cycles_per_job_cu || !ms || jobs < 8) return -1;
+    switch (which) {
+        case 0: return run<131, 81, 15>(device, jobs, cycles_per_job_cu, ms);
+        case 1: return run<131, 0, 0>(device, jobs, cycles_per_job_cu, ms);
+        case 2: return run<0, 81, 0>(device, jobs, cycles_per_job_cu, ms);
+        case 3: return run<0, 0, 15>(device, jobs, cycles_per_job_cu, ms);
+        default: return -1;
+    }
+}
+
 }  // extern "C"

@@ -15,7 +15,7 @@
 // write; no intermediate deblocked plane exists.
 //
 // Edge information comes from dbk_map_kernel: one byte per 8x8 luma block,
-//   bits 0..5 QpY of its CU, bit 6 its left side is a transform-block edge,
+//   bits 0..5 Qp'Y of its CU (= QpY at 8 bits; loopfilter16.h subtracts QpBdOffsetY), bit 6 its left side is a transform-block edge,
 //   bit 7 its top side is a transform-block edge.
 // In 4:2:0 intra pictures every TB boundary on the 8x8 grid is an edge with bS = 2
 // (8.7.2.4: intra on either side); prediction-block edges of NxN CUs sit at 4-sample
@@ -61,11 +61,10 @@ __global__ __launch_bounds__(64) void dbk_map_kernel(const DevPic* __restrict__ 
     const p265r_ctu me = P->ctus[blockIdx.x];
     const p265r_tb* tbs = P->tbs + me.tb_begin;
     uint8_t* map = P->dbk_map;
-    const int qp_off = 6 * (g.bd[0] - 8);
     for (int t = threadIdx.x; t < me.tb_count; t += 64) {
         const p265r_tb tb = tbs[t];
         if (tb.c_idx != 0) continue;
-        const int qpy = (int)tb.qp - qp_off;
+        const int qpy = (int)tb.qp;                  // Qp'Y (0..63 up to BitDepth 10)
         const int bx0 = tb.x >> 3, by0 = tb.y >> 3;
         if (tb.log2_size == 2) {
             if ((tb.x & 7) == 0 && (tb.y & 7) == 0) map[by0 * g.nf_w + bx0] = (uint8_t)(qpy | DBK_V | DBK_H);

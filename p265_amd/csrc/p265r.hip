@@ -27,6 +27,7 @@
 #include "intra_prep.h"
 #include "intra_rows.h"
 #include "loopfilter.h"
+#include "loopfilter16.h"
 #include "residual.h"
 #include "sao.h"
 #include "sao_strip16.h"
@@ -501,7 +502,10 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     *out = nullptr;
     const p265r_params& p = *params;
     if (!params_ok(p)) return P265R_EINVAL;
-    if (p.bit_depth_luma != 8 || p.bit_depth_chroma != 8 || p.scaling_list_enabled) return P265R_EUNSUPPORTED;
+    // BitDepth 8 (uint8_t planes, the row pipeline) or 9..10 with one depth for luma and chroma (Main 10:
+    // uint16_t planes, the per-diagonal intra kernel and loopfilter16.h)
+    if (p.bit_depth_luma < 8 || p.bit_depth_luma > 10 || p.bit_depth_chroma != p.bit_depth_luma || p.scaling_list_enabled)
+        return P265R_EUNSUPPORTED;
     const int n = p265r_device_count();
     if (n < 0) return n;
     if (device < 0 || device >= n) return P265R_ENODEV;
@@ -518,6 +522,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     g.wc = (g.w + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
     g.hc = (g.h + (1 << g.ctb_log2) - 1) >> g.ctb_log2;
     g.bd[0] = p.bit_depth_luma; g.bd[1] = g.bd[2] = p.bit_depth_chroma;
+    g.pel16 = p.bit_depth_luma > 8 ? 1 : 0;
     g.strong = p.strong_intra_smoothing;
     g.lf_tiles = p.loop_filter_across_tiles;
     g.nf_w = (g.w + 7) / 8;
@@ -535,6 +540,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
                           "P265R_FORK_PREP", "P265R_SPLIT", "P265R_XG", "P265R_TR_CHECK"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
+    if (g.pel16) ctx->schedule = 0;          // 16-bit samples: the per-diagonal intra kernel
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';
@@ -699,7 +705,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         for (int rs = 0; rs < pnc[i]; ++rs)
             if (pics[i].ctus[rs].flags & P265R_CTU_DEBLOCK) { dbk = true; break; }
     const bool lf = sao || dbk;                  // separate output planes
-    const size_t plane_bytes[3] = {(size_t)g.stride[0] * g.h, (size_t)g.stride[1] * g.ch, (size_t)g.stride[2] * g.ch};
+    const size_t pb = g.pel16 ? 2 : 1;          // bytes per sample
+    const size_t plane_bytes[3] = {(size_t)g.stride[0] * g.h * pb, (size_t)g.stride[1] * g.ch * pb, (size_t)g.stride[2] * g.ch * pb};
     const size_t pic_plane_bytes = align_up(plane_bytes[0], 256) + 2 * align_up(plane_bytes[1], 256);
     size_t off = 0;
     const size_t o_pics = off; off = align_up(off + sizeof(DevPic) * n_pics, 256);
@@ -918,7 +925,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         for (int i = 0; i < n_pics && e == hipSuccess; ++i)
             for (int c = 0; c < 3 && e == hipSuccess; ++c) {
                 const int wd[3] = {psize[i][0], psize[i][0] / 2, psize[i][0] / 2}, ht[3] = {psize[i][1], psize[i][1] / 2, psize[i][1] / 2};
-                e = hipMemcpy2DAsync(b->h_pics[i].rec[c], g.stride[c], pics[i].recon[c], wd[c], wd[c], ht[c],
+                e = hipMemcpy2DAsync(b->h_pics[i].rec[c], g.stride[c] * pb, pics[i].recon[c], wd[c] * pb, wd[c] * pb, ht[c],
                                      hipMemcpyHostToDevice, st);
             }
     }
@@ -1110,7 +1117,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         const int cy_max = std::min(g.hc - 1, step / 2);
         if (cy_max < cy_min) continue;
         dim3 grid(cy_max - cy_min + 1, b->n_pics);
-        intra_step_kernel<<<grid, 64, 0, s>>>(b->d_pics, b->d_pool, b->d_res, g, step, cy_min);
+        if (g.pel16) intra_step_kernel<uint16_t><<<grid, 64, 0, s>>>(b->d_pics, b->d_pool, b->d_res, g, step, cy_min);
+        else intra_step_kernel<uint8_t><<<grid, 64, 0, s>>>(b->d_pics, b->d_pool, b->d_res, g, step, cy_min);
         ++tm.intra_launches;
     }
     HIP_TRY(hipGetLastError());
@@ -1139,7 +1147,23 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         s = ctx->aux[li];
         HIP_TRY(hipStreamWaitEvent(s, b->intra_done, 0));
     }
-    if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && g.h % 8 == 0 && !(skip & 4)) {
+    if (g.pel16 && (b->dbk || b->sao) && !(skip & 4)) {
+        // 16-bit samples (Main 10): deblocking + SAO in loopfilter16.h, with or without deblocking
+        const long long units = (long long)ctx->n_ctus * b->n_pics;
+        if (units >= (1ll << 31) - 8) return P265R_ERANGE;
+        const dim3 grid((unsigned)((units + 7) / 8 * 8));
+        const int so = b->sao ? 1 : 0, np = b->n_pics;
+        switch (g.ctb_log2 * 2 + (b->dbk ? 1 : 0)) {
+            case 12: loopfilter16_kernel<6, false><<<grid, 256, 0, s>>>(b->d_pics, g, so, np); break;
+            case 13: loopfilter16_kernel<6, true><<<grid, 256, 0, s>>>(b->d_pics, g, so, np); break;
+            case 10: loopfilter16_kernel<5, false><<<grid, 256, 0, s>>>(b->d_pics, g, so, np); break;
+            case 11: loopfilter16_kernel<5, true><<<grid, 256, 0, s>>>(b->d_pics, g, so, np); break;
+            case 8: loopfilter16_kernel<4, false><<<grid, 256, 0, s>>>(b->d_pics, g, so, np); break;
+            default: loopfilter16_kernel<4, true><<<grid, 256, 0, s>>>(b->d_pics, g, so, np); break;
+        }
+        ++tm.sao_launches;
+        HIP_TRY(hipGetLastError());
+    } else if (b->sao && !b->dbk && ctx->sao_rows == 1 && g.ctb_log2 >= 5 && g.h % 8 == 0 && !(skip & 4)) {
         // SAO only, CTB 32 / 64: the 16-samples-per-lane strip kernel (sao_strip16.h), one wave per
         // (picture, CTB row, component, 992-sample strip), 4 waves per block, blocks dealt XCD-aware;
         // it filters 4-row chunks and takes plane heights in multiples of 4 (luma a multiple of
@@ -1205,11 +1229,12 @@ int p265r_batch_download(p265r_ctx* ctx, p265r_batch* b, const p265r_picture* pi
     // planes to copy: (host destination, device source, row pitch, width, height)
     struct Item { void* dst; const unsigned char* src; int pitch, w, h; size_t bytes; };
     std::vector<Item> items;
+    const int pb = g.pel16 ? 2 : 1;                          // bytes per sample
     for (int i = 0; i < n_pics; ++i)
         for (int c = 0; c < 3; ++c) {
             const int sub = c ? 1 : 0;
-            const int w = b->size[i][0] >> sub, h = b->size[i][1] >> sub;
-            const int pitch = c ? g.stride[1] : g.stride[0];
+            const int w = (b->size[i][0] >> sub) * pb, h = b->size[i][1] >> sub;     // (w in bytes)
+            const int pitch = (c ? g.stride[1] : g.stride[0]) * pb;
             if (pics[i].out[c]) items.push_back({pics[i].out[c], b->h_pics[i].out[c], pitch, w, h, (size_t)w * h});
             if (pics[i].recon[c] && !b->recon_input)
                 items.push_back({pics[i].recon[c], b->h_pics[i].rec[c], pitch, w, h, (size_t)w * h});
@@ -1437,7 +1462,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
         "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"xg\": %d, \"last_launch_xg\": %d, "
-        "\"phase_order\": %d, \"row_launches\": {\"w12\": %lld, \"w8\": %lld, \"w16_split\": %lld, \"xg\": %lld, \"other\": %lld}, "
+        "\"phase_order\": %d, \"bit_depth\": %d, \"row_launches\": {\"w12\": %lld, \"w8\": %lld, \"w16_split\": %lld, \"xg\": %lld, \"other\": %lld}, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : (P265R_PHASE_ORDER
@@ -1458,7 +1483,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         0,
 #endif
         P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, ctx->xg, ctx->last_xg ? 1 : 0, P265R_PHASE_ORDER,
-        ctx->row_launches[0], ctx->row_launches[1], ctx->row_launches[2], ctx->row_launches[3], ctx->row_launches[4],
+        (int)ctx->params.bit_depth_luma, ctx->row_launches[0], ctx->row_launches[1], ctx->row_launches[2], ctx->row_launches[3], ctx->row_launches[4],
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;
     if (size > 0) {

@@ -18,6 +18,15 @@
 
 namespace p265r {
 
+#ifndef P265R_RES_NT
+#define P265R_RES_NT 0   // A/B: residual stores non-temporal (the row kernel reads them a phase later)
+#endif
+typedef unsigned int res_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void res_store16(int16_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if constexpr (P265R_RES_NT) __builtin_nontemporal_store(res_u4{a, b, c, d}, reinterpret_cast<res_u4*>(p));
+    else *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+}
+
 struct ResJob {          // 8 bytes, one per coded TB, in pool order within its class
     uint32_t off;        // int16 offset of the TB in the pool
     uint8_t  qp;         // qP (incl. QpBdOffset)
@@ -128,8 +137,8 @@ __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restric
         o[y * 2 + 0] = (uint32_t)(uint16_t)r[0] | ((uint32_t)(uint16_t)r[1] << 16);
         o[y * 2 + 1] = (uint32_t)(uint16_t)r[2] | ((uint32_t)(uint16_t)r[3] << 16);
     }
-    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<uint4*>(dst + 8) = make_uint4(o[4], o[5], o[6], o[7]);
+    res_store16(dst, o[0], o[1], o[2], o[3]);
+    res_store16(dst + 8, o[4], o[5], o[6], o[7]);
 }
 
 // ---------------------------------------------------------------------------
@@ -305,7 +314,7 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
                 }
                 o[h] = (uint32_t)(uint16_t)r2[0] | ((uint32_t)(uint16_t)r2[1] << 16);
             }
-            *reinterpret_cast<uint4*>(dst + lane * N + v * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+            res_store16(dst + lane * N + v * 8, o[0], o[1], o[2], o[3]);
         }
     }
 }

@@ -56,6 +56,10 @@ __device__ __forceinline__ void expand_mask(uint32_t m16, uint32_t* d) {
 #define P265R_SAO_WPE 6
 #endif
 
+#ifndef P265R_SAO_NT
+#define P265R_SAO_NT 0                     // A/B: 1 non-temporal output stores, 2 non-temporal loads too
+#endif
+
 constexpr int kSao16Strip = 62 * 16;       // output samples per strip
 #ifndef P265R_SAO16_CHUNK
 #define P265R_SAO16_CHUNK 2
@@ -112,7 +116,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
     const int yb = cy << Ls, ye = min(yb + cs, H);
     const int bx = Xc >> Ls, xb = bx << Ls;
     auto row_ld = [&](int y) {
-        return *(const __attribute__((address_space(1))) u4v*)(src + __umul24((uint32_t)min(max(y, 0), H - 1), (uint32_t)st) + Xc);
+        const __attribute__((address_space(1))) u4v* p =
+            (const __attribute__((address_space(1))) u4v*)(src + __umul24((uint32_t)min(max(y, 0), H - 1), (uint32_t)st) + Xc);
+        if constexpr (P265R_SAO_NT >= 2) return __builtin_nontemporal_load(p);
+        else return *p;
     };
     // ---- first: the rows of the first chunk (position only) ----------------------------------
     constexpr int K = kSao16Chunk;
@@ -276,8 +283,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P265R_SAO_W
                     const uint32_t mk = m[j] & ~nfm[j];
                     out[j] = (res & mk) | (cur & ~mk);
                 }
-                if (act && y < ye)
-                    *(__attribute__((address_space(1))) u4v*)(dst + __umul24((uint32_t)y, (uint32_t)st) + Xc) = u4v{out[0], out[1], out[2], out[3]};
+                if (act && y < ye) {
+                    __attribute__((address_space(1))) u4v* q = (__attribute__((address_space(1))) u4v*)(dst + __umul24((uint32_t)y, (uint32_t)st) + Xc);
+                    if constexpr (P265R_SAO_NT >= 1) __builtin_nontemporal_store(u4v{out[0], out[1], out[2], out[3]}, q);
+                    else *q = u4v{out[0], out[1], out[2], out[3]};
+                }
             }
             rowv[0] = rowv[K];
             rowv[1] = rowv[K + 1];

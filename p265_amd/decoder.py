@@ -33,7 +33,7 @@ class DecodedFrame:
     poc: int
     output_rank: int
     decode_index: int
-    planes: list                 # full decoded Y, Cb, Cr (uint8, pic_width x pic_height)
+    planes: list                 # full decoded Y, Cb, Cr (uint8; uint16 above 8 bits), pic_width x pic_height
     crop: tuple                  # (left, right, top, bottom) luma samples
     hash_ok: Optional[bool]      # None: stream carries no picture hash for this picture
 

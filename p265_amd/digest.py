@@ -1,8 +1,9 @@
 """Host restatement of the device picture digest (p265r_batch_digest, csrc/digest.h).
 
-digest(plane) = sum over the plane's 4-sample words (row y, word k, W/4 words per row) of
-mix64(word | (y * W/4 + k) << 32) mod 2^64, with mix64 the splitmix64 finalizer and word the
-little-endian 32-bit value of samples 4k..4k+3 of row y.  Position-keyed, so a changed, swapped
+digest(plane) = sum over the plane's 32-bit words (row y, word k, K words per row) of
+mix64(word | (y * K + k) << 32) mod 2^64, with mix64 the splitmix64 finalizer and word the
+little-endian 32-bit value of the row's bytes 4k..4k+3: samples 4k..4k+3 of a uint8 plane (K = W/4),
+samples 2k, 2k+1 of a uint16 plane (BitDepth > 8, K = W/2).  Position-keyed, so a changed, swapped
 or shifted sample changes it; a sum, so the device adds partial sums in any order.
 """
 import numpy as np
@@ -18,8 +19,10 @@ def _mix64(z):
 
 
 def plane_digest(plane):
-    """Digest of one uint8 plane [h][w] (w a multiple of 4) as a Python int."""
-    p = np.ascontiguousarray(plane, np.uint8)
+    """Digest of one plane [h][w] (w a multiple of 4) as a Python int: a uint16 plane as 16-bit samples
+    (BitDepth > 8), anything else as uint8 samples (8-bit planes; the oracle's integer arrays)."""
+    p = np.asarray(plane)
+    p = np.ascontiguousarray(p, "<u2" if p.dtype == np.uint16 else np.uint8)
     h, w = p.shape
     if w % 4:
         raise ValueError("plane width %d is not a multiple of 4" % w)
@@ -30,5 +33,5 @@ def plane_digest(plane):
 
 
 def picture_digest(planes):
-    """[Y, Cb, Cr] uint8 planes -> uint64 array of 3 digests (p265r_batch_digest's layout)."""
+    """[Y, Cb, Cr] planes -> uint64 array of 3 digests (p265r_batch_digest's layout)."""
     return np.array([plane_digest(pl) for pl in planes], np.uint64)

@@ -4,7 +4,7 @@ Mirrors what the reference's reconstruction hook would do per picture
 (decoder/cu.py:483-494 -> decode_intra, decoder/sao.py), but per batch:
 
     ctx = ReconContext(params, device=0)
-    frames = ctx.decode([pic0, pic1, ...])          # -> [(Y, Cb, Cr), ...] uint8 planes
+    frames = ctx.decode([pic0, pic1, ...])          # -> [(Y, Cb, Cr), ...] planes (uint8; uint16 > 8 bits)
 
 or, keeping inputs resident in HBM (the benchmark path):
 
@@ -43,7 +43,8 @@ class DecodedPicture:
     before the in-loop filters (pu.reconstructed_samples, reconstruction.py:25), which is what
     intra prediction of later blocks reads.  ``get_output_sample`` returns the decoded
     (deblocked + SAO) sample that is written out.  ``planes`` / ``recon`` are [Y, Cb, Cr]
-    uint8 arrays indexed [y][x] (the reference's arrays are x-major [x][y])."""
+    arrays indexed [y][x] (the reference's arrays are x-major [x][y]): uint8 at BitDepth 8, uint16
+    above (Main 10)."""
 
     def __init__(self, planes, recon):
         self.planes, self.recon = planes, recon
@@ -135,7 +136,8 @@ class ReconContext:
                     c.recon[k] = recons[i][k].ctypes.data
             if p.recon_input is not None:
                 c.flags = R.PIC_RECON_INPUT
-                planes = [np.ascontiguousarray(p.recon_input[k], np.uint8) for k in range(3)]
+                dts = R.plane_dtypes(self.params)
+                planes = [np.ascontiguousarray(p.recon_input[k], dts[k]) for k in range(3)]
                 for k, (pl, shp) in enumerate(zip(planes, plane_shapes(pp))):
                     if pl.shape != shp:
                         raise R.RecordError("recon_input plane %d has shape %s, expected %s" % (k, pl.shape, shp))
@@ -144,7 +146,8 @@ class ReconContext:
         return arr, keep
 
     def _alloc_planes(self, pics):
-        return [[np.empty(s, np.uint8) for s in plane_shapes(R.pic_params(self.params, p))] for p in pics]
+        dts = R.plane_dtypes(self.params)
+        return [[np.empty(s, dt) for s, dt in zip(plane_shapes(R.pic_params(self.params, p)), dts)] for p in pics]
 
     # ---- batch API --------------------------------------------------------------
     def upload(self, pics):
@@ -162,8 +165,9 @@ class ReconContext:
         n = len(batch.pics)
         sel = set(range(n)) if only is None else {int(i) for i in only}
         shp = [plane_shapes(R.pic_params(self.params, p)) for p in batch.pics]
-        outs = [[np.empty(s, np.uint8) for s in shp[i]] if i in sel else None for i in range(n)]
-        recs = ([[np.empty(s, np.uint8) for s in shp[i]] if i in sel else None for i in range(n)]
+        dts = R.plane_dtypes(self.params)
+        outs = [[np.empty(s, dt) for s, dt in zip(shp[i], dts)] if i in sel else None for i in range(n)]
+        recs = ([[np.empty(s, dt) for s, dt in zip(shp[i], dts)] if i in sel else None for i in range(n)]
                 if with_recon else None)
         arr = (_lib.PictureC * n)()
         for i in sel:

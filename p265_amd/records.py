@@ -64,6 +64,19 @@ def make_params(**kw) -> np.ndarray:
     return p
 
 
+def plane_dtypes(params):
+    """numpy sample type of the Y, Cb, Cr planes: uint8 at BitDepth 8, uint16 (little-endian) above
+    (include/p265r.h p265r_picture.out / recon)."""
+    dy = np.uint8 if int(params["bit_depth_luma"]) <= 8 else np.uint16
+    dc = np.uint8 if int(params["bit_depth_chroma"]) <= 8 else np.uint16
+    return [dy, dc, dc]
+
+
+def qp_bd_offset(params, c_idx=0) -> int:
+    """QpBdOffsetY / QpBdOffsetC = 6 * (BitDepth - 8) (7.4.3.2.1)."""
+    return 6 * (int(params["bit_depth_luma" if c_idx == 0 else "bit_depth_chroma"]) - 8)
+
+
 def deblock_offsets(beta_offset_div2, tc_offset_div2) -> int:
     """P265R_DEBLOCK_OFFSETS: two 4-bit two's-complement fields (each -6..6)."""
     for v in (beta_offset_div2, tc_offset_div2):

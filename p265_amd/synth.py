@@ -12,6 +12,11 @@ Deblocking is considered disabled (the SAO input is the reconstruction).
 ``perf=True`` uses the mode histogram of sanity.bin and QP 32; ``perf=False`` (parity)
 uses uniform modes 0..34, QP 22..37, random strong-smoothing-prone flat areas and
 optional multiple slices / tiles.
+
+Above 8 bits (params bit_depth_luma / _chroma, Main 10) the records carry qP' = QpY + QpBdOffset
+(parity pictures draw QpY from -QpBdOffsetY.. as well), SAO offsets use the whole
+sao_offset_abs range (cMax = (1 << (Min(BitDepth, 10) - 5)) - 1) and PCM samples the whole
+sample range; at 8 bits every random draw is the one it always was.
 """
 import numpy as np
 
@@ -89,11 +94,14 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
         slice_dbk = {s: (bool(deblocking), 0, 0) for s in first}
     max_tb = int(p["max_tb_log2_size"])
     flat_bias = 0.0 if perf else 0.3
+    bdy, bdc = int(p["bit_depth_luma"]), int(p["bit_depth_chroma"])
+    offy, offc = R.qp_bd_offset(p, 0), R.qp_bd_offset(p, 1)
 
     def qps():
-        qy = 32 if perf else int(rng.integers(22, 38))
-        qcb, qcr = frontend.chroma_qp(qy, 0, 0)
-        return qy, qcb, qcr
+        # QpY, then qP' of each component (+ QpBdOffset): what the TB records carry
+        qy = 32 if perf else int(rng.integers(22 - offy, 38))
+        qcb, qcr = frontend.chroma_qp(qy, 0, 0, offc)
+        return qy + offy, qcb + offc, qcr + offc
 
     def mode():
         return int(rng.choice(35, p=_MODE_P)) if perf else int(rng.integers(0, 35))
@@ -147,7 +155,8 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
         qy, qcb, qcr = qps()
         if pcm_rate > 0 and log2 <= 5 and rng.random() < pcm_rate:
             n = 1 << log2
-            smp = [rng.integers(0, 256, (n >> (c > 0), n >> (c > 0))).astype(np.int16) for c in range(3)]
+            smp = [rng.integers(0, 1 << (bdy if c == 0 else bdc), (n >> (c > 0), n >> (c > 0))).astype(np.int16)
+                   for c in range(3)]
             b.add_cu(x, y, log2, 0, [0] * 4, 0, qy, qcb, qcr, [], pcm=True, pcm_samples=smp)
             return
         nxn = log2 == 3 and rng.random() < 0.41
@@ -170,7 +179,7 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
             typ[0] = 0 if r < 0.02 else (1 if r < 0.18 else 2)
             r = rng.random()
             typ[1] = typ[2] = 0 if r < 0.3 else (1 if r < 0.5 else 2)
-            ab = rng.integers(0, 8, (3, 4))
+            ab = rng.integers(0, 1 << (min(max(bdy, bdc), 10) - 5), (3, 4))     # 0..cMax
             sg = rng.integers(0, 2, (3, 4))
             band = rng.integers(0, 32, 3)
             eo = rng.integers(0, 4, 3)

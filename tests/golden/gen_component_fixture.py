@@ -21,7 +21,12 @@ This script feeds them seeded random inputs, stores inputs + the reference's out
 in tests/golden/ref_components.npz, and asserts at generation time that the tables of
 oracle/recon_oracle.py equal the reference's (transform.py:5-72, intra.py:15-22).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python3 -B tests/golden/gen_component_fixture.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python3 -B tests/golden/gen_component_fixture.py [--bit-depth 10]
+
+--bit-depth 10 (Main 10) writes ref_components_bd10.npz / .json: the same functions with the SPS's
+BitDepthY = BitDepthC = 10 and QpBdOffset = 12 (scaling.py:14-26 bdShift and qP, reconstruction.py:25
+and utils.py:11-15 clip, intra.py:241 substitution default, intra.py:280-281 strong-filter threshold,
+intra.py:160 edge-filter clip), samples 0..1023 and QpY -12..51.  The 8-bit run is unchanged.
 """
 import contextlib
 import hashlib
@@ -57,7 +62,7 @@ def _md(neigh):
     return d
 
 
-def main():
+def main(bd=8):
     mods = _refshim.install("/tmp/p265_component_fixture")
     _refshim.silence(mods)
     intra, scaling, transform, recon = mods["intra"], mods["scaling"], mods["transform"], mods["reconstruction"]
@@ -69,8 +74,12 @@ def main():
     assert list(intra.IntraPu.inv_angle_table) == O.INV_ANGLE
 
     rng = np.random.default_rng(SEED)
-    sps = _NS(bit_depth_y=8, bit_depth_c=8, strong_intra_smoothing_enabled_flag=1, qp_bd_offset_y=0,
-              qp_bd_offset_c=0, scaling_list_enabled_flag=0)
+    sh = bd - 8                                        # sample ranges scale with the bit depth (0 at 8 bits)
+    off = 6 * sh                                       # QpBdOffsetY / QpBdOffsetC
+    mx = (1 << bd) - 1
+    dt = np.uint8 if bd == 8 else np.uint16
+    sps = _NS(bit_depth_y=bd, bit_depth_c=bd, strong_intra_smoothing_enabled_flag=1, qp_bd_offset_y=off,
+              qp_bd_offset_c=off, scaling_list_enabled_flag=0)
 
     # ---- prediction ----------------------------------------------------------------
     modes_ok = [0, 1] + list(range(2, 18)) + [18, 26]
@@ -83,12 +92,12 @@ def main():
             c_idx = 1
         style = case % 3                    # smooth ramps / random / near-flat
         if style == 0:
-            base = rng.integers(0, 200)
-            L = np.clip(base + np.cumsum(rng.integers(-3, 4, 4 * n + 1)), 0, 255)
+            base = rng.integers(0, 200 << sh)
+            L = np.clip(base + np.cumsum(rng.integers(-3, 4, 4 * n + 1)), 0, mx)
         elif style == 1:
-            L = rng.integers(0, 256, 4 * n + 1)
+            L = rng.integers(0, mx + 1, 4 * n + 1)
         else:
-            L = np.clip(128 + rng.integers(-2, 3, 4 * n + 1), 0, 255)
+            L = np.clip((128 << sh) + rng.integers(-2, 3, 4 * n + 1), 0, mx)
         cu = _NS(ctx=_NS(sps=sps))
         pu = intra.IntraPu(cu, c_idx, mode, int(np.log2(n)), 0, 0)
         nb = _md(L)
@@ -98,9 +107,9 @@ def main():
             pu.decode_intra_dc(nb, 0, 0, int(np.log2(n)))
         else:
             pu.decode_intra_angular(nb, 0, 0, int(np.log2(n)))
-        out = np.zeros((32, 32), np.uint8)
+        out = np.zeros((32, 32), dt)
         out[:n, :n] = np.asarray(pu.predicted_samples).T        # -> [y][x]
-        Lp = np.zeros(129, np.uint8)
+        Lp = np.zeros(129, dt)
         Lp[: 4 * n + 1] = L
         P_n.append(n); P_mode.append(mode); P_c.append(c_idx); P_L.append(Lp); P_out.append(out)
 
@@ -123,9 +132,9 @@ def main():
             avail[0] = False
         style = case % 2
         if style == 0:
-            vals = np.clip(rng.integers(20, 230) + np.cumsum(rng.integers(-1, 2, m)), 0, 255)
+            vals = np.clip(rng.integers(20 << sh, 230 << sh) + np.cumsum(rng.integers(-1, 2, m)), 0, mx)
         else:
-            vals = rng.integers(0, 256, m)
+            vals = rng.integers(0, mx + 1, m)
         dx, dy = O.ref_positions(n)
         x0 = y0 = 64
         lut = {(x0 + int(a), y0 + int(b)): (bool(av), int(v)) for a, b, av, v in zip(dx, dy, avail, vals)}
@@ -139,14 +148,14 @@ def main():
             nb = pu.decode_neighbor(x0, y0, int(np.log2(n)), 0)
         got = np.array([nb[int(a)][int(b)] for a, b in zip(dx, dy)], np.int64)
         pad = lambda a, dt: np.pad(np.asarray(a, dt), (0, 129 - m))
-        F_n.append(n); F_mode.append(mode); F_avail.append(pad(avail, np.uint8)); F_vals.append(pad(vals, np.uint8))
-        F_out.append(pad(got, np.uint8))
+        F_n.append(n); F_mode.append(mode); F_avail.append(pad(avail, np.uint8)); F_vals.append(pad(vals, dt))
+        F_out.append(pad(got, dt))
 
     # ---- scaling ---------------------------------------------------------------------
     S_n, S_qp, S_c, S_lvl, S_out = [], [], [], [], []
     for case in range(240):
         n = [4, 8, 16, 32][case % 4]
-        qp = int(rng.integers(0, 52))
+        qp = int(rng.integers(-off, 52))                  # QpY; the reference adds QpBdOffset (scaling.py:14-18)
         c_idx = int(rng.integers(0, 3))
         lvl = np.zeros((n, n), np.int64)
         mask = rng.random((n, n)) < 0.3
@@ -163,11 +172,11 @@ def main():
         out[:n, :n] = np.asarray(pu.scaled_samples).T
         lp = np.zeros((32, 32), np.int16)
         lp[:n, :n] = lvl
-        S_n.append(n); S_qp.append(qp); S_c.append(c_idx); S_lvl.append(lp); S_out.append(out)
+        S_n.append(n); S_qp.append(qp + off); S_c.append(c_idx); S_lvl.append(lp); S_out.append(out)   # qP
 
     # ---- reconstruction clip -----------------------------------------------------------
-    R_pred = rng.integers(0, 256, (64, 8, 8))
-    R_res = rng.integers(-300, 300, (64, 8, 8))
+    R_pred = rng.integers(0, mx + 1, (64, 8, 8))
+    R_res = rng.integers(-300 << sh, 300 << sh, (64, 8, 8))
     R_out = []
     for i in range(64):
         cu = _NS(ctx=_NS(sps=sps))
@@ -175,9 +184,10 @@ def main():
         pu.predicted_samples[:] = R_pred[i].T
         pu.transformed_samples[:] = R_res[i].T
         recon.reconstruction(pu, 0, 0, 3)
-        R_out.append(np.asarray(pu.reconstructed_samples).T.astype(np.uint8))
+        R_out.append(np.asarray(pu.reconstructed_samples).T.astype(dt))
 
-    out = os.path.join(HERE, "ref_components.npz")
+    tag = "" if bd == 8 else "_bd%d" % bd
+    out = os.path.join(HERE, "ref_components%s.npz" % tag)
     np.savez_compressed(
         out,
         pred_n=np.array(P_n, np.uint8), pred_mode=np.array(P_mode, np.uint8), pred_c=np.array(P_c, np.uint8),
@@ -186,17 +196,20 @@ def main():
         filt_vals=np.array(F_vals), filt_out=np.array(F_out),
         scal_n=np.array(S_n, np.uint8), scal_qp=np.array(S_qp, np.uint8), scal_c=np.array(S_c, np.uint8),
         scal_level=np.array(S_lvl), scal_out=np.array(S_out),
-        rec_pred=R_pred.astype(np.uint8), rec_res=R_res.astype(np.int16), rec_out=np.array(R_out))
+        rec_pred=R_pred.astype(dt), rec_res=R_res.astype(np.int16), rec_out=np.array(R_out))
     meta = dict(generator="tests/golden/gen_component_fixture.py", seed=SEED,
                 tables_match_reference=["transform.py:5 DST4", "transform.py:7-72 DCT32",
                                         "intra.py:15-18 intraPredAngle", "intra.py:19-22 invAngle"],
                 cases=dict(pred=len(P_n), filter=len(F_n), scaling=len(S_n), reconstruction=64),
-                bit_depth=8, strong_intra_smoothing=1,
+                bit_depth=bd, strong_intra_smoothing=1,
                 npz_sha256=hashlib.sha256(open(out, "rb").read()).hexdigest())
-    with open(os.path.join(HERE, "ref_components.json"), "w") as f:
+    with open(os.path.join(HERE, "ref_components%s.json" % tag), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print(json.dumps(meta, indent=1))
 
 
 if __name__ == "__main__":
-    main()
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 10))
+    main(ap.parse_args().bit_depth)

@@ -8,6 +8,9 @@
   bench.py's front-end / end-to-end legs (config C3 from real bytes).
 * synth_4k_tiles.bin -- config C5 from a real bitstream: 3840x2160, 2x2 uniform tiles,
   2 pictures, loop filters not across tiles, SAO.
+* synth_main10.bin -- Main 10: 416x240, BitDepth 10, 3 IDR pictures, CTB 64, cu_qp_delta (QpY
+  down to -QpBdOffsetY), PCM at 9 / 8 bits, SAO offsets up to cMax 31, deblocking with per-slice
+  overrides over two slices; MD5 over 16-bit little-endian samples.
 Each picture is followed by a decoded-picture-hash SEI (MD5) of the C oracle's decode of
 the generator's records, so any decode of these files is self-checking.
 """
@@ -32,6 +35,9 @@ FIXTURES = {
     "synth_1080p_4pic.bin": dict(seed=1080, width=1920, height=1080, frames=4, idr_period=1, **STATS),
     "synth_4k_tiles.bin": dict(seed=2160, width=3840, height=2160, frames=2, idr_period=1, tiles=(2, 2),
                                lf_across_tiles=0, **STATS),
+    "synth_main10.bin": dict(seed=1010, width=416, height=240, frames=3, idr_period=1, bit_depth=10,
+                             qp_delta_depth=1, pcm=(3, 4, True), deblocking="override",
+                             slices=[(0, False), (12, False)], **dict(STATS, init_qp=20, slice_qp_delta=4)),
 }
 
 

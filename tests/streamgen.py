@@ -264,6 +264,7 @@ DEFAULTS = dict(
     frames=1, idr_period=0, log2_max_poc_lsb=8, poc_order=None, max_reorder=0,   # poc_order: POC per frame (IDR first)
     split_prob=0.55, tf_split_prob=0.5, nxn_prob=0.4, cbf_prob=0.7, chroma_cbf_prob=0.35, pcm_prob=0.08,
     bypass_prob=0.1, tskip_prob=0.3, density=0.25, big_prob=0.03,
+    bit_depth=8,                # BitDepthY = BitDepthC (8, or 9..10: Main 10 -- QpBdOffset, SAO cMax, PCM depths)
 )
 
 
@@ -284,7 +285,11 @@ class StreamGen:
             pic_width=self.W, pic_height=self.H, ctb_log2_size=c["ctb_log2"], min_tb_log2_size=c["min_tb_log2"],
             max_tb_log2_size=c["max_tb_log2"], strong_intra_smoothing=int(c["strong"]),
             sample_adaptive_offset=int(c["sao"]), loop_filter_across_tiles=int(c["lf_across_tiles"]) if c["tiles"] else 1,
-            pps_cb_qp_offset=c["cb_qp_offset"], pps_cr_qp_offset=c["cr_qp_offset"])
+            pps_cb_qp_offset=c["cb_qp_offset"], pps_cr_qp_offset=c["cr_qp_offset"],
+            bit_depth_luma=c["bit_depth"], bit_depth_chroma=c["bit_depth"])
+        self.bd = c["bit_depth"]
+        self.qp_off = 6 * (self.bd - 8)                  # QpBdOffsetY = QpBdOffsetC
+        self.pcm_bd = (8, 7) if self.bd == 8 else (self.bd - 1, self.bd - 2)
 
     # tile structure (6.5.1)
     def _tiles(self):
@@ -331,8 +336,9 @@ class StreamGen:
         return nal(32, bw.bytes())
 
     def _ptl(self, bw):
-        bw.u(0, 2); bw.u(0, 1); bw.u(1, 5)            # Main profile
-        bw.u(0x60000000, 32)
+        main10 = self.cfg["bit_depth"] > 8
+        bw.u(0, 2); bw.u(0, 1); bw.u(2 if main10 else 1, 5)     # Main / Main 10 profile
+        bw.u(0x20000000 if main10 else 0x60000000, 32)
         bw.u(0b1001, 4)
         bw.u(0, 43); bw.u(0, 1)
         bw.u(120, 8)
@@ -350,7 +356,7 @@ class StreamGen:
                 bw.ue(v)
         else:
             bw.u(0, 1)
-        bw.ue(0); bw.ue(0)                               # bit depths 8
+        bw.ue(self.bd - 8); bw.ue(self.bd - 8)           # bit_depth_luma / chroma_minus8
         bw.ue(c["log2_max_poc_lsb"] - 4)
         bw.u(1, 1); bw.ue(1 + c["max_reorder"]); bw.ue(c["max_reorder"]); bw.ue(0)
         bw.ue(c["min_cb_log2"] - 3); bw.ue(c["ctb_log2"] - c["min_cb_log2"])
@@ -360,7 +366,7 @@ class StreamGen:
         bw.u(1, 1); bw.u(int(c["sao"]), 1)               # amp, sao
         if c["pcm"]:
             lo, hi, lfd = c["pcm"]
-            bw.u(1, 1); bw.u(7, 4); bw.u(6, 4)             # PcmBitDepth 8 / 7
+            bw.u(1, 1); bw.u(self.pcm_bd[0] - 1, 4); bw.u(self.pcm_bd[1] - 1, 4)   # PcmBitDepth Y / C
             bw.ue(lo - 3); bw.ue(hi - lo); bw.u(int(lfd), 1)
         else:
             bw.u(0, 1)
@@ -679,12 +685,13 @@ class StreamGen:
                     types[ci] = t
                     if not t:
                         continue
+                    cmax = (1 << (min(self.bd, 10) - 5)) - 1     # sao_offset_abs: TR, cMax by bit depth
                     for i in range(4):
-                        a = int(r.integers(0, 8))
+                        a = int(r.integers(0, cmax + 1))
                         sao["abs"][ci][i] = a
                         for _ in range(a):
                             enc.bypass(1)
-                        if a < 7:
+                        if a < cmax:
                             enc.bypass(0)
                     if t == 1:
                         for i in range(4):
@@ -779,12 +786,13 @@ class StreamGen:
             self.ipm[y0 >> 2:(y0 + size) >> 2, x0 >> 2:(x0 + size) >> 2] = 1
             self.enc.bw.align_zero()                     # pcm_alignment_zero_bit(s) after the flush
             pcm_samples = []
-            for ci, (lg, bd) in enumerate(((log2, 8), (log2 - 1, 7), (log2 - 1, 7))):
+            pby, pbc = self.pcm_bd
+            for ci, (lg, bd) in enumerate(((log2, pby), (log2 - 1, pbc), (log2 - 1, pbc))):
                 n = 1 << lg
                 v = r.integers(0, 1 << bd, (n, n))
                 for s in v.reshape(-1):
                     self.enc.bw.u(int(s), bd)
-                pcm_samples.append((v << (8 - bd)).astype(np.int16))
+                pcm_samples.append((v << (self.bd - bd)).astype(np.int16))
             self.enc.start()
         else:
             nparts = 4 if nxn else 1
@@ -828,13 +836,14 @@ class StreamGen:
                     mode_c = 34
             self.cu = dict(x=x0, y=y0, log2=log2, nxn=nxn, bypass=bypass, modes=modes, mode_c=mode_c)
             self._tt(x0, y0, x0, y0, log2, 0, 0, 1, 1, tus)
-        qpy = ((self.qg_pred + self.qp_delta + 52) % 52)
+        off = self.qp_off                                # QpY (8.6.1), then qP' = Qp + QpBdOffset for the records
+        qpy = ((self.qg_pred + self.qp_delta + 52 + 2 * off) % (52 + off)) - off
         self.last_qp = qpy
         self.qpmap[y0 >> mcb:(y0 + size) >> mcb, x0 >> mcb:(x0 + size) >> mcb] = qpy
         h = self.h
-        qcb = qpc_of(min(max(qpy + c["cb_qp_offset"] + h["cb"], 0), 57))
-        qcr = qpc_of(min(max(qpy + c["cr_qp_offset"] + h["cr"], 0), 57))
-        self.builder.add_cu(x0, y0, log2, 1 if nxn else 0, modes, mode_c, qpy, qcb, qcr, tus,
+        qcb = qpc_of(min(max(qpy + c["cb_qp_offset"] + h["cb"], -off), 57))
+        qcr = qpc_of(min(max(qpy + c["cr_qp_offset"] + h["cr"], -off), 57))
+        self.builder.add_cu(x0, y0, log2, 1 if nxn else 0, modes, mode_c, qpy + off, qcb + off, qcr + off, tus,
                             bypass=bool(bypass), pcm=bool(pcm), pcm_samples=pcm_samples)
 
     def _tt(self, x0, y0, xb, yb, log2, depth, blk, pcb, pcr, tus):
@@ -863,7 +872,7 @@ class StreamGen:
         enc.decision(self._ctx("cbf_luma", 1 if depth == 0 else 0), cbl)
         ccb, ccr = (cb, cr) if log2 > 2 else (pcb, pcr)
         if (cbl or ccb or ccr) and c["qp_delta_depth"] is not None and not self.qp_delta_coded:
-            lim = 26
+            lim = 26 + self.qp_off // 2                  # CuQpDeltaVal in -(26 + QpBdOffsetY / 2) .. 25 + QpBdOffsetY / 2
             v = int(r.integers(-lim, lim)) if r.random() < 0.7 else 0
             # bias towards the small values of real streams but keep large ones for the EG0 suffix
             if r.random() < 0.6:
@@ -1101,15 +1110,19 @@ def sei_nal(payload, nal_type=40, payload_type=132):
 
 
 def picture_hash(planes, kind):
-    """Decoded picture hash per component (D.3.19): md5 / crc / checksum of 8-bit planes."""
+    """Decoded picture hash per component (D.3.19): md5 / crc / checksum of 8-bit planes, or of 16-bit
+    planes (BitDepth > 8: pictureData holds every sample as two bytes, little-endian; the checksum adds
+    (sample >> 8) ^ xorMask per sample too)."""
     out = []
     for c, p in enumerate(planes):
-        p = np.ascontiguousarray(p, np.uint8)
+        p = np.ascontiguousarray(p)
+        wide = p.dtype == np.uint16
+        p = p.astype("<u2") if wide else p.astype(np.uint8)
         if kind == "md5":
             out.append(hashlib.md5(p.tobytes()).digest())
         elif kind == "crc":
             crc = 0xFFFF
-            for b in p.reshape(-1):
+            for b in np.frombuffer(p.tobytes(), np.uint8):
                 for i in range(8):
                     msb = (crc >> 15) & 1
                     bit = (int(b) >> (7 - i)) & 1
@@ -1122,6 +1135,8 @@ def picture_hash(planes, kind):
             h, w = p.shape
             ys, xs = np.mgrid[0:h, 0:w]
             xm = (xs & 0xFF) ^ (ys & 0xFF) ^ (xs >> 8) ^ (ys >> 8)
-            s = int(np.sum((p.astype(np.int64) ^ xm) & 0xFF)) & 0xFFFFFFFF
-            out.append(s.to_bytes(4, "big"))
+            s = int(np.sum((p.astype(np.int64) & 0xFF) ^ xm))
+            if wide:
+                s += int(np.sum((p.astype(np.int64) >> 8) ^ xm))
+            out.append((s & 0xFFFFFFFF).to_bytes(4, "big"))
     return out

@@ -59,9 +59,10 @@ def test_invalid_params_rejected_before_device():
     h = ctypes.c_void_p()
     assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EINVAL      # version 0
     p.version, p.pic_width, p.pic_height, p.chroma_format_idc = 2, 64, 64, 1
-    p.bit_depth_luma = p.bit_depth_chroma = 10
     p.ctb_log2_size, p.min_tb_log2_size, p.max_tb_log2_size = 6, 2, 5
-    assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EUNSUPPORTED  # 10-bit
+    for bl, bc in ((12, 12), (10, 8), (8, 9), (7, 7)):        # Main 10: one depth of 8..10 for luma and chroma
+        p.bit_depth_luma, p.bit_depth_chroma = bl, bc
+        assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EUNSUPPORTED
     assert lib.p265r_wait(None) == _lib.EINVAL
 
 
@@ -93,3 +94,11 @@ def test_front_end_exports_every_declared_symbol():
     assert lib.p265fe_create(ctypes.byref(h)) == 0
     assert lib.p265fe_picture(h, 0, None) == bitstream.EINVAL
     lib.p265fe_destroy(h)
+
+
+def test_probe_library_exports_its_measurement_entry_points():
+    """libp265probe.so (bench.py's measurement helper, not the product path): the issue-ceiling and the
+    HBM stream-rate probes."""
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(HEADER)), "p265_amd", "libp265probe.so"))
+    for name in ("p265probe_issue", "p265probe_stream"):
+        assert hasattr(lib, name), name

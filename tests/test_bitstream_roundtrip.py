@@ -38,6 +38,12 @@ CASES = {
     "ctb32_mincb16": dict(ctb_log2=5, min_cb_log2=4, max_tb_log2=5, max_th_depth=3),
     "poc_idr_period": dict(frames=4, idr_period=3, log2_max_poc_lsb=4),
     "lf_flags_off": dict(lf_across_tiles=0, tiles=(2, 1), lf_across_slices=0),
+    # Main 10: bit_depth_*_minus8 = 2, QpBdOffset 12 (cu_qp_delta range, QpY wrap, negative QpY), sao_offset_abs
+    # cMax 31, PCM at 9 / 8 bits shifted to 10
+    "main10": dict(bit_depth=10, qp_delta_depth=1, init_qp=14, slice_qp_delta=-20, pcm=(3, 4, True)),
+    "main10_tiles_wpp_bypass": dict(bit_depth=10, tiles=(2, 2), wpp=True, bypass=True, qp_delta_depth=0),
+    "main9_chroma_offsets": dict(bit_depth=9, slice_chroma_offsets=(3, -5), cb_qp_offset=-4, cr_qp_offset=6,
+                                 qp_delta_depth=1, deblocking="override", slices=[(0, False), (20, False)]),
 }
 
 
@@ -80,9 +86,10 @@ def test_conformance_window_and_counts():
     assert dec[0].n_slices == 1 and dec[0].n_cus > 0
 
 
+@pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("kind", ["md5", "crc", "checksum"])
-def test_decoded_picture_hash_sei_is_reported(kind):
-    g = streamgen.StreamGen(11, hash_sei=kind)
+def test_decoded_picture_hash_sei_is_reported(kind, bd):
+    g = streamgen.StreamGen(11, hash_sei=kind, bit_depth=bd)
     data, pics = g.stream()
     dec = bitstream.decode_stream(data)
     want_type, want = g.last_hash
@@ -108,3 +115,16 @@ def test_unsupported_and_missing_parameter_sets():
     # truncated slice data
     with pytest.raises(bitstream.BitstreamError):
         bitstream.decode_stream(data[:len(data) - 40])
+
+
+@pytest.mark.parametrize("kind", ["md5", "crc", "checksum"])
+def test_hash_of_16bit_planes_matches_the_encoder(kind):
+    """bitstream.plane_hash (the decoder's D.3.19 check) of uint16 planes equals the test encoder's
+    independent restatement (streamgen.picture_hash): two bytes per sample, the checksum's high byte."""
+    from p265_amd import bitstream as B
+    rng = np.random.default_rng(4)
+    planes = [rng.integers(0, 1024, (40, 24)).astype(np.uint16), rng.integers(0, 1024, (20, 12)).astype(np.uint16),
+              rng.integers(0, 1024, (20, 12)).astype(np.uint16)]
+    want = streamgen.picture_hash(planes, kind)
+    code = {"md5": B.HASH_MD5, "crc": B.HASH_CRC, "checksum": B.HASH_CHECKSUM}[kind]
+    assert [B.plane_hash(p, code) for p in planes] == want

@@ -44,3 +44,17 @@ def test_synthetic(ctb_log2, w, h, tiles, slices):
 def test_no_sao():
     params = R.make_params(pic_width=128, pic_height=64, sample_adaptive_offset=0, strong_intra_smoothing=0)
     _same(params, [synth.make_picture(params, 9, perf=False)])
+
+
+@pytest.mark.parametrize("ctb_log2,w,h,tiles,slices", [(6, 200, 136, (1, 1), 1), (5, 264, 200, (3, 2), 4), (4, 72, 40, (1, 1), 2)])
+def test_synthetic_main10(ctb_log2, w, h, tiles, slices):
+    """BitDepth 10 (Main 10; uint16 planes): scaling / clip / substitution / SAO band shift / deblocking
+    thresholds and QpY = qP' - 12, with deblocking on random slices, PCM, bypass, transform skip."""
+    params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2, loop_filter_across_tiles=int(w % 3 == 0),
+                           bit_depth_luma=10, bit_depth_chroma=10, pps_cb_qp_offset=-2, pps_cr_qp_offset=3)
+    pics = [synth.make_picture(params, 1700 + s, perf=bool(s), tiles=tiles, n_slices=slices, lf_across_slices=None,
+                               tskip_rate=0.3, bypass_rate=0.05, pcm_rate=0.03, deblocking="random") for s in range(2)]
+    assert max(int(pics[0].tbs["qp"].max()), int(pics[1].tbs["qp"].max())) > 37     # qP' = QpY + 12 (QpY <= 37)
+    _same(params, pics)
+    got = c_oracle.decode(params, pics[:1])[0][1]
+    assert got[0].dtype == np.uint16 and got[0].max() > 255

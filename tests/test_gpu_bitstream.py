@@ -54,6 +54,9 @@ CASES = {
     "lf_off_tiles": dict(tiles=([2, 6], [3, 3]), lf_across_tiles=0, lf_across_slices=0,
                          slices=[(0, False), (30, False)]),
     "multi_frame": dict(frames=3, idr_period=2),
+    "main10": dict(bit_depth=10, pcm=(3, 4, True), bypass=True, qp_delta_depth=1, init_qp=14, slice_qp_delta=-18,
+                   deblocking="override", slices=[(0, False), (20, False)]),
+    "main10_tiles_wpp_ctb32": dict(bit_depth=10, tiles=(2, 2), wpp=True, ctb_log2=5, width=192, height=128),
 }
 
 
@@ -95,9 +98,17 @@ def test_cli_writes_cropped_yuv(dec_mod, tmp_path):
     raw = np.frombuffer(out.read_bytes(), np.uint8)
     want = oracle_planes(*pics[0][:2])[0][6:6 + h, 2:2 + w]
     np.testing.assert_array_equal(raw[:w * h].reshape(h, w), want)
+    # Main 10: 16-bit little-endian samples (yuv420p10le)
+    g = streamgen.StreamGen(79, hash_sei="md5", bit_depth=10, width=136, height=104, frames=1)
+    data, pics = g.stream(planes_fn=oracle_planes)
+    src.write_bytes(data)
+    assert dec.main(["-b", str(src), "-o", str(out)]) == 0
+    assert out.stat().st_size == 2 * (136 * 104 * 3 // 2)
+    raw = np.frombuffer(out.read_bytes(), "<u2")
+    np.testing.assert_array_equal(raw[:136 * 104].reshape(104, 136), oracle_planes(*pics[0][:2])[0])
 
 
-@pytest.mark.parametrize("name", ["synth_1080p_4pic.bin", "synth_4k_tiles.bin"])
+@pytest.mark.parametrize("name", ["synth_1080p_4pic.bin", "synth_4k_tiles.bin", "synth_main10.bin"])
 def test_committed_streams_match_their_md5(dec_mod, name):
     data = open(os.path.join(GOLDEN, name), "rb").read()
     frames = dec_mod.decode_bytes(data)                     # raises HashMismatch on any difference

@@ -1,0 +1,109 @@
+"""Main 10 (BitDepth 10) on the GPU through the C ABI vs the oracles, bit-exact.
+
+The 16-bit sample path (uint16_t planes; per-diagonal intra kernel intra_step_kernel<uint16_t>,
+loopfilter16.h; the residual kernels with bdShift = BitDepth + log2 - 5 and 20 - BitDepth) against
+oracle/recon_oracle.py (pinned at 10 bits by tests/golden/ref_components_bd10.npz from the reference's
+own scaling / prediction / reconstruction, tests/test_oracle_vs_reference.py) and its C twin.
+"""
+import numpy as np
+import pytest
+
+from oracle import c_oracle
+from oracle import recon_oracle as O
+from p265_amd import digest, synth
+from p265_amd import records as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def recon_mod():
+    from p265_amd import recon
+    if recon.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    return recon
+
+
+def _check(recon_mod, params, pics, label, c_ref=False):
+    with recon_mod.ReconContext(params) as ctx:
+        assert ctx.describe()["bit_depth"] == int(params["bit_depth_luma"])
+        outs, recs = ctx.decode(pics, with_recon=True)
+    if c_ref:
+        refs = c_oracle.decode(params, pics, threads=8)
+    else:
+        pd = R.params_dict(params)
+        refs = [O.decode_picture(R.params_dict(R.pic_params(params, p)), p.as_oracle_dict()) for p in pics]
+    for i in range(len(pics)):
+        for c in range(3):
+            assert outs[i][c].dtype == np.uint16
+            np.testing.assert_array_equal(recs[i][c], refs[i][0][c], err_msg="%s pic %d recon c%d" % (label, i, c))
+            np.testing.assert_array_equal(outs[i][c], refs[i][1][c], err_msg="%s pic %d out c%d" % (label, i, c))
+    return outs
+
+
+@pytest.mark.parametrize("ctb_log2,w,h,deblocking", [(6, 352, 288, False), (5, 200, 136, "random"), (4, 72, 40, True),
+                                                     (6, 136, 72, "random")])
+def test_main10_uniform_modes(recon_mod, ctb_log2, w, h, deblocking):
+    params = R.make_params(pic_width=w, pic_height=h, ctb_log2_size=ctb_log2, bit_depth_luma=10, bit_depth_chroma=10,
+                           pps_cb_qp_offset=(w % 5) - 2, pps_cr_qp_offset=2 - (h % 5))
+    pics = [synth.make_picture(params, 5100 + 10 * ctb_log2 + s, perf=False, deblocking=deblocking) for s in range(3)]
+    _check(recon_mod, params, pics, "main10 uniform")
+
+
+def test_main10_slices_tiles_pcm_bypass_tskip(recon_mod):
+    params = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, loop_filter_across_tiles=0,
+                           bit_depth_luma=10, bit_depth_chroma=10)
+    pics = [synth.make_picture(params, 5200 + s, perf=False, tiles=(3, 2), n_slices=4, lf_across_slices=None,
+                               deblocking="random", bypass_rate=0.05, pcm_rate=0.03, tskip_rate=0.3) for s in range(2)]
+    _check(recon_mod, params, pics, "main10 tiles")
+
+
+def test_main10_no_sao(recon_mod):
+    params = R.make_params(pic_width=128, pic_height=64, sample_adaptive_offset=0, bit_depth_luma=10, bit_depth_chroma=10)
+    _check(recon_mod, params, [synth.make_picture(params, 5300 + s, perf=False) for s in range(2)], "main10 nosao")
+    params = R.make_params(pic_width=128, pic_height=64, sample_adaptive_offset=0, bit_depth_luma=10, bit_depth_chroma=10)
+    _check(recon_mod, params, [synth.make_picture(params, 5310, perf=False, deblocking=True)], "main10 dbk only")
+
+
+def test_main10_1080p_with_deblocking(recon_mod):
+    params = R.make_params(pic_width=1920, pic_height=1080, bit_depth_luma=10, bit_depth_chroma=10)
+    pics = [synth.make_picture(params, 5400 + s, perf=True, deblocking=bool(s)) for s in range(2)]
+    _check(recon_mod, params, pics, "main10 1080p", c_ref=True)
+
+
+def test_main10_9bit(recon_mod):
+    params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5, bit_depth_luma=9, bit_depth_chroma=9)
+    pics = [synth.make_picture(params, 5500 + s, perf=False, deblocking="random", pcm_rate=0.02) for s in range(2)]
+    _check(recon_mod, params, pics, "9-bit")
+
+
+def test_main10_ragged_batch_and_digest(recon_mod):
+    """A ragged 10-bit batch (four picture sizes) and the device digest of uint16 planes (32-bit words of two
+    samples) equal the host digest of the oracle's planes."""
+    big = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, bit_depth_luma=10, bit_depth_chroma=10)
+    sizes = [(264, 200), (128, 72), (40, 200), (264, 8)]
+    pics = []
+    for k, (w, h) in enumerate(sizes):
+        pp = R.pic_params(big, R.Picture(ctus=None, tbs=None, coef=None, size=(w, h)))
+        pic = synth.make_picture(pp, 5600 + k, perf=bool(k % 2), deblocking=True)
+        pic.size = (w, h)
+        pics.append(pic)
+    _check(recon_mod, big, pics, "main10 ragged")
+    with recon_mod.ReconContext(big) as ctx:
+        b = ctx.upload(pics)
+        ctx.run(b)
+        got, got_rec = ctx.digest(b), ctx.digest(b, recon=True)
+        b.free()
+    for i, pic in enumerate(pics):
+        rec_ref, out_ref = O.decode_picture(R.params_dict(R.pic_params(big, pic)), pic.as_oracle_dict())
+        assert np.array_equal(got[i], digest.picture_digest([np.asarray(p, np.uint16) for p in out_ref])), "out %d" % i
+        assert np.array_equal(got_rec[i], digest.picture_digest([np.asarray(p, np.uint16) for p in rec_ref])), "rec %d" % i
+
+
+def test_unsupported_bit_depths_rejected(recon_mod):
+    from p265_amd import _lib
+    for bl, bc in ((12, 12), (10, 8), (8, 10)):
+        params = R.make_params(pic_width=64, pic_height=64, bit_depth_luma=bl, bit_depth_chroma=bc)
+        with pytest.raises(_lib.P265RError) as ei:
+            recon_mod.ReconContext(params)
+        assert ei.value.code == _lib.EUNSUPPORTED

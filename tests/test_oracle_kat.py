@@ -230,3 +230,53 @@ def test_sao_edge_offset_local_min_max_and_picture_edge():
     assert out[5, 5] == 43 and out[7, 7] == 57 and out[9, 0] == 10
     assert out[5, 4] == 50 - 1 and out[5, 6] == 50 - 1        # edgeIdx 3 (greater than one neighbour) -> -1
     assert out[2, 2] == 50                                    # flat -> edgeIdx 0
+
+
+# ---------------------------------------------------------------------------------
+# Main 10 (BitDepth 10): hand-worked cases of the bit-depth-dependent steps
+# ---------------------------------------------------------------------------------
+
+def test_dequant_10bit_equals_8bit_at_qp_plus_qpbdoffset():
+    # 8.6.3: d = (L * 16 * levelScale[qP % 6] << (qP / 6) + (1 << (bdShift - 1))) >> bdShift with
+    # bdShift = BitDepth + log2 - 5: at BitDepth 10 and qP' = qP + 12 both shifts grow by 2 -- same d
+    rng = np.random.default_rng(10)
+    for log2 in (2, 3, 4, 5):
+        lvl = rng.integers(-3000, 3000, (1 << log2, 1 << log2))
+        for qp in range(0, 52, 3):
+            np.testing.assert_array_equal(O.dequantize(lvl, qp + 12, log2, 10), O.dequantize(lvl, qp, log2, 8))
+
+
+def test_dc_only_residual_10bit():
+    # L = 1 at (0, 0), qP' 16, 4x4 DCT (chroma): d = (16 * 64 << 2 + 64) >> 7 = 32; stage 1: (64 * 32 + 64) >> 7
+    # = 16; stage 2 (bdShift 20 - 10 = 10): (64 * 16 + 512) >> 10 = 1 in every sample (at 8 bits: 0)
+    lvl = np.zeros((4, 4), np.int64)
+    lvl[0, 0] = 1
+    np.testing.assert_array_equal(O.residual_block(lvl, 2, 1, 16, 0x01, 10), np.ones((4, 4)))
+    np.testing.assert_array_equal(O.residual_block(lvl, 2, 1, 4, 0x01, 8), np.zeros((4, 4)))
+
+
+def test_sao_band_offset_10bit():
+    # bandShift = BitDepth - 5 = 5: bands of 32 sample values; SaoOffsetVal as coded (shift 10 - Min(10, 10) = 0)
+    params, pic = _one_ctb_pic(1, 4, [1, 2, 3, 31])
+    params.update(bit_depth_luma=10, bit_depth_chroma=10)
+    v = (np.arange(256).reshape(16, 16) * 4).astype(np.int64)          # 0 .. 1020
+    rec = [v, np.zeros((8, 8), np.int64), np.zeros((8, 8), np.int64)]
+    out = O.sao_picture(params, pic, rec)[0]
+    exp = v + np.select([(v >> 5) == 4, (v >> 5) == 5, (v >> 5) == 6, (v >> 5) == 7], [1, 2, 3, 31], 0)
+    np.testing.assert_array_equal(out, exp)
+    from p265_amd import frontend
+    assert frontend.sao_offset_val(1, [31, 2, 0, 5], [1, 0, 0, 1], 10) == [-31, 2, 0, -5]
+
+
+def test_deblocking_thresholds_scale_with_bit_depth():
+    # QpY 37 on both sides: beta' = 2 * 37 - 38 = 36, tC' = 4 (Q = 39).  A P side bent by 20 per line:
+    # d = 40 >= 36 -> no filtering at 8 bits; at 10 bits beta = 144 -> filtered (8.7.2.5.3)
+    p = [[100, 100, 100, 100], [110, 110, 110, 110], [100, 100, 100, 100], [100, 100, 100, 100]]
+    q = [[104] * 4, [104] * 4, [104] * 4, [104] * 4]
+    p8, q8 = O.deblock_luma_segment(p, q, 37, 37, 0, 0, False, False, 8)
+    assert p8 == p and q8 == q
+    p10, q10 = O.deblock_luma_segment(p, q, 37, 37, 0, 0, False, False, 10)
+    assert p10 != p or q10 != q
+    # chroma: QpC = Table 8-10(37) = 34, tC' = TC_TABLE[36] = 4, x 4 at 10 bits
+    assert O.chroma_tc(37, 37, 0, 0, 8) == O.TC_TABLE[O.qpc_from_qpi(37) + 2] == 4
+    assert O.chroma_tc(37, 37, 0, 0, 10) == 16
