@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define P265FE_ABI_VERSION 3u   /* 3: P265FE_ASYNC, p265fe_wait */
+#define P265FE_ABI_VERSION 4u   /* 3: P265FE_ASYNC, p265fe_wait; 4: scaling_factors */
 
 #define P265FE_OK            0
 #define P265FE_EINVAL       -1   /* bad argument                                   */
@@ -82,6 +82,10 @@ typedef struct p265fe_picture_info {
     uint8_t          max_num_reorder; /* sps_max_num_reorder_pics: output "bumping" (C.5.2.2)   */
     uint8_t          output_flag;   /* PicOutputFlag                                             */
     uint16_t         reserved;
+    const uint8_t*   scaling_factors; /* params.scaling_list_enabled: the intra ScalingFactor table of
+                                       its SPS / PPS (7.4.5; PPS lists, else SPS lists, else the
+                                       defaults), P265R_SCALING_FACTOR_BYTES in the layout of
+                                       p265r_set_scaling_factors; NULL otherwise                  */
 } p265fe_picture_info;
 
 typedef struct p265fe_pictures p265fe_pictures;

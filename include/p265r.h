@@ -73,8 +73,8 @@ typedef struct p265r_params {
     uint16_t pic_width;               /* pic_width_in_luma_samples                */
     uint16_t pic_height;              /* pic_height_in_luma_samples               */
     uint8_t  chroma_format_idc;       /* 1 (4:2:0) only                           */
-    uint8_t  bit_depth_luma;          /* 8 only in this version                   */
-    uint8_t  bit_depth_chroma;        /* 8 only in this version                   */
+    uint8_t  bit_depth_luma;          /* BitDepthY: 8, or 9..10 (Main 10: uint16_t planes) */
+    uint8_t  bit_depth_chroma;        /* BitDepthC: equal to bit_depth_luma        */
     uint8_t  ctb_log2_size;           /* CtbLog2SizeY, 4..6                       */
     uint8_t  min_tb_log2_size;        /* MinTbLog2SizeY, 2..5                     */
     uint8_t  max_tb_log2_size;        /* MaxTbLog2SizeY, <= 5                     */
@@ -82,7 +82,9 @@ typedef struct p265r_params {
     uint8_t  constrained_intra_pred;  /* constrained_intra_pred_flag (no effect: all-intra) */
     uint8_t  sample_adaptive_offset;  /* sample_adaptive_offset_enabled_flag      */
     uint8_t  loop_filter_across_tiles;/* loop_filter_across_tiles_enabled_flag    */
-    uint8_t  scaling_list_enabled;    /* must be 0 in this version                */
+    uint8_t  scaling_list_enabled;    /* scaling_list_enabled_flag: 1 = dequantise with the ScalingFactor
+                                         table given by p265r_set_scaling_factors (sps.py:86-90,
+                                         scaling.py:32-44)                          */
     int8_t   pps_cb_qp_offset;        /* cQpPicOffset of Cb chroma deblocking (8.7.2.5.5) */
     int8_t   pps_cr_qp_offset;        /* cQpPicOffset of Cr chroma deblocking     */
     uint8_t  reserved[11];
@@ -214,6 +216,15 @@ int  p265r_sync(p265r_ctx* ctx);
  * runtime accepts at most 32, so past depth 15 such batches share hardware queues).
  * Runs of one batch stay ordered; p265r_sync waits for every stream.  Default 1. */
 int  p265r_set_pipeline(p265r_ctx* ctx, int depth);
+/* Scaling lists (scaling_list_enabled = 1; decoder/scaling.py:32-44, m[x][y] = ScalingFactor[sizeId]
+ * [matrixId][x][y]): the intra ScalingFactor arrays, 2032 bytes, each matrix row-major m[y][x] (y the
+ * row): 4x4 Y, Cb, Cr at byte 0, 16, 32; 8x8 Y, Cb, Cr at 48, 112, 176; 16x16 Y, Cb, Cr at 240, 496,
+ * 752 (DC included); 32x32 Y at 1008 -- the derivation of 7.4.5 from the SPS / PPS scaling_list_data
+ * (default lists included) is the caller's (libp265fe.so delivers it with every picture).  Values
+ * 1..255.  Applies to every later run of the context (waits for the runs in flight first); a context
+ * with scaling_list_enabled refuses to run (P265R_ESTATE) until it is set. */
+#define P265R_SCALING_FACTOR_BYTES 2032
+int  p265r_set_scaling_factors(p265r_ctx* ctx, const uint8_t* factors, int n_bytes);
 /* Measurement knob (no counterpart in the reference): force the intra row kernel's build for this
  * context's later runs -- 8 or 12 waves per workgroup -- or 0 (default) to pick it per run (12 for a
  * batch alone, 8 beside other lanes' runs, the latency layouts for small batches).  Lets a benchmark

@@ -22,12 +22,16 @@ def load():
         _lib = ctypes.CDLL(LIB)
         _lib.oracle_decode.restype = ctypes.c_int
         _lib.oracle_decode.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(PictureC), ctypes.c_int, ctypes.c_int]
+        _lib.oracle_decode_sl.restype = ctypes.c_int
+        _lib.oracle_decode_sl.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.POINTER(PictureC), ctypes.c_int,
+                                          ctypes.c_int]
     return _lib
 
 
-def decode(params, pics, threads=0, with_recon=True):
+def decode(params, pics, threads=0, with_recon=True, scaling=None):
     """[(recon planes, out planes)] for each picture, computed by the C oracle.  Pictures with a
-    size of their own (Picture.size, a ragged batch) are decoded with their own parameter set."""
+    size of their own (Picture.size, a ragged batch) are decoded with their own parameter set.
+    ``scaling``: the 2032-byte intra ScalingFactor array when params.scaling_list_enabled."""
     groups = {}
     for i, p in enumerate(pics):
         pp = R.pic_params(params, p)
@@ -35,13 +39,13 @@ def decode(params, pics, threads=0, with_recon=True):
     if len(groups) > 1 or (groups and next(iter(groups.values()))[0] is not params):
         res = [None] * len(pics)
         for pp, idx in groups.values():
-            for i, r in zip(idx, _decode(pp, [pics[i] for i in idx], threads, with_recon)):
+            for i, r in zip(idx, _decode(pp, [pics[i] for i in idx], threads, with_recon, scaling)):
                 res[i] = r
         return res
-    return _decode(params, pics, threads, with_recon)
+    return _decode(params, pics, threads, with_recon, scaling)
 
 
-def _decode(params, pics, threads, with_recon):
+def _decode(params, pics, threads, with_recon, scaling=None):
     lib = load()
     pc = Params()
     for name, _ in Params._fields_:
@@ -71,7 +75,10 @@ def _decode(params, pics, threads, with_recon):
             if with_recon:
                 a.recon[k] = rec[k].ctypes.data
         res.append((rec, out))
-    rc = lib.oracle_decode(ctypes.byref(pc), arr, len(pics), int(threads))
+    sf = None if scaling is None else np.ascontiguousarray(scaling, np.uint8)
+    if sf is not None and sf.size != 2032:
+        raise ValueError("scaling factors: 2032 bytes expected, got %d" % sf.size)
+    rc = lib.oracle_decode_sl(ctypes.byref(pc), None if sf is None else sf.ctypes.data, arr, len(pics), int(threads))
     if rc:
         raise RuntimeError("oracle_decode failed: %d" % rc)
     return res

@@ -96,8 +96,8 @@ static int available(const geo_t* g, int xc, int yc, int xn, int yn) {
     return 1;
 }
 
-/* residual r[y*n+x] of one TB (8.6.2-8.6.4) */
-static void residual(const int16_t* lvl, int log2, int c, int qp, int flags, int bd, int* r) {
+/* residual r[y*n+x] of one TB (8.6.2-8.6.4); m: the TB's ScalingFactor m[y*n+x] (NULL: flat 16) */
+static void residual(const int16_t* lvl, int log2, int c, int qp, int flags, int bd, const uint8_t* m, int* r) {
     const int n = 1 << log2, nn = n * n;
     if (flags & (P265R_TB_BYPASS | P265R_TB_PCM)) {
         for (int i = 0; i < nn; ++i) r[i] = lvl[i];
@@ -106,7 +106,7 @@ static void residual(const int16_t* lvl, int log2, int c, int qp, int flags, int
     int d[1024];
     const int bds = bd + log2 - 5;
     for (int i = 0; i < nn; ++i) {
-        long long v = ((long long)lvl[i] * 16 * LEVEL_SCALE[qp % 6]) << (qp / 6);
+        long long v = ((long long)lvl[i] * (m ? m[i] : 16) * LEVEL_SCALE[qp % 6]) << (qp / 6);
         d[i] = clip3(-32768, 32767, (v + (1LL << (bds - 1))) >> bds);
     }
     const int bd2 = 20 - bd;
@@ -189,7 +189,14 @@ static void predict(const int* p, int n, int mode, int c, int bd, int* pred) {
  * uint8_t for BitDepth 8 and uint16_t (little-endian) above (p265r_picture). */
 typedef uint16_t pel;
 
-static void recon_tb(const geo_t* g, const p265r_params* prm, pel* planes[3], const int stride[3],
+/* byte offset of the intra ScalingFactor of (log2 size, component) in the 2032-byte array
+ * (include/p265r.h p265r_set_scaling_factors) */
+static int sf_offset(int log2, int c) {
+    static const int OFF[4][3] = {{0, 16, 32}, {48, 112, 176}, {240, 496, 752}, {1008, -1, -1}};
+    return OFF[log2 - 2][c];
+}
+
+static void recon_tb(const geo_t* g, const p265r_params* prm, const uint8_t* sf, pel* planes[3], const int stride[3],
                      const p265r_tb* t, const int16_t* coef) {
     const int c = t->c_idx, log2 = t->log2_size, n = 1 << log2, sub = c ? 1 : 0;
     const int bd = c ? prm->bit_depth_chroma : prm->bit_depth_luma;
@@ -198,7 +205,8 @@ static void recon_tb(const geo_t* g, const p265r_params* prm, pel* planes[3], co
     pel* pl = planes[c];
     const int st = stride[c];
     int res[1024], pred[1024];
-    if (t->flags & (P265R_TB_CBF | P265R_TB_PCM)) residual(coef + t->coef_off, log2, c, t->qp, t->flags, bd, res);
+    if (t->flags & (P265R_TB_CBF | P265R_TB_PCM))
+        residual(coef + t->coef_off, log2, c, t->qp, t->flags, bd, sf ? sf + sf_offset(log2, c) : NULL, res);
     else memset(res, 0, sizeof(int) * n * n);
     if (t->flags & P265R_TB_PCM) {
         memset(pred, 0, sizeof(int) * n * n);
@@ -474,10 +482,13 @@ static void plane_out(void* dst, const pel* src, size_t n, int bd) {
     else for (size_t i = 0; i < n; ++i) ((uint8_t*)dst)[i] = (uint8_t)src[i];
 }
 
-/* Decode n pictures: writes pics[i].recon[] (if set) and pics[i].out[] (if set).
+/* Decode n pictures: writes pics[i].recon[] (if set) and pics[i].out[] (if set).  sf: the intra
+ * ScalingFactor arrays (2032 bytes, layout of p265r_set_scaling_factors) when scaling_list_enabled.
  * Returns 0 or a negative P265R_* code.  n_threads <= 0: OpenMP default. */
-int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int n_threads) {
+int oracle_decode_sl(const p265r_params* prm, const uint8_t* sf, const p265r_picture* pics, int n, int n_threads) {
     if (!prm || !pics || n < 0) return P265R_EINVAL;
+    if (prm->scaling_list_enabled && !sf) return P265R_EINVAL;
+    if (!prm->scaling_list_enabled) sf = NULL;
     if (prm->bit_depth_luma < 8 || prm->bit_depth_luma > 12 || prm->bit_depth_chroma < 8 || prm->bit_depth_chroma > 12 ||
         prm->chroma_format_idc != 1)
         return P265R_EUNSUPPORTED;
@@ -507,7 +518,7 @@ int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int
         for (int ts = 0; ts < nc; ++ts) {
             const p265r_ctu* cu = &pics[i].ctus[order[ts]];
             for (uint32_t k = cu->tb_begin; k < cu->tb_begin + cu->tb_count; ++k)
-                recon_tb(&g, prm, rec, stride, &pics[i].tbs[k], pics[i].coef);
+                recon_tb(&g, prm, sf, rec, stride, &pics[i].tbs[k], pics[i].coef);
         }
         for (int c = 0; c < 3; ++c)
             if (pics[i].recon[c]) plane_out(pics[i].recon[c], rec[c], sz[c], bd[c]);
@@ -535,4 +546,8 @@ int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int
         free(rs2ts);
     }
     return err ? P265R_EINVAL : P265R_OK;
+}
+
+int oracle_decode(const p265r_params* prm, const p265r_picture* pics, int n, int n_threads) {
+    return oracle_decode_sl(prm, NULL, pics, n, n_threads);
 }

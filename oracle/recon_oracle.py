@@ -75,6 +75,114 @@ INV_ANGLE = [-4096, -1638, -910, -630, -482, -390, -315, -256, -315, -390, -482,
 LEVEL_SCALE = [40, 45, 51, 57, 64, 72]   # scaling.py:28
 
 TB_CBF, TB_TSKIP, TB_BYPASS, TB_PCM = 1, 2, 4, 8
+
+# ---------------------------------------------------------------------------
+# Scaling lists (7.3.4 syntax, 7.4.5 semantics / ScalingFactor derivation) -- the ScalingFactor
+# branch of decoder/scaling.py:32-44 (m[x][y] = sps.scaling_factor[size_id][matrix_id][x][y]).
+# The reference's list derivation (sld.py) is broken, its default tables are data:
+# Table 7-6 below equals sld.py:13-33 (tests/test_scaling_lists.py).
+# ---------------------------------------------------------------------------
+SL_DEFAULT_8X8_INTRA = [16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 16, 17, 16, 17, 18, 17, 18, 18, 17, 18, 21, 19,
+                        20, 21, 20, 19, 21, 24, 22, 22, 24, 24, 22, 22, 24, 25, 25, 27, 30, 27, 25, 25, 29, 31, 35,
+                        35, 31, 29, 36, 41, 44, 41, 36, 47, 54, 54, 47, 65, 70, 65, 88, 88, 115]
+SL_DEFAULT_8X8_INTER = [16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 17, 18, 18, 18, 18, 18, 18, 20, 20,
+                        20, 20, 20, 20, 20, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 28, 28, 28,
+                        28, 28, 28, 33, 33, 33, 33, 33, 41, 41, 41, 41, 54, 54, 54, 71, 71, 91]
+# ABI layout of the intra ScalingFactor arrays (include/p265r.h p265r_set_scaling_factors): m[y][x] per
+# (sizeId, matrixId): 4x4 Y/Cb/Cr, 8x8 Y/Cb/Cr, 16x16 Y/Cb/Cr, 32x32 Y; 2032 bytes
+SF_OFFSETS = {(0, 0): 0, (0, 1): 16, (0, 2): 32, (1, 0): 48, (1, 1): 112, (1, 2): 176,
+              (2, 0): 240, (2, 1): 496, (2, 2): 752, (3, 0): 1008}
+SF_BYTES = 2032
+
+
+def diag_scan(blk):
+    """6.5.3 up-right diagonal scan of a blk x blk block: [(x, y)] in scan order."""
+    out, x, y = [], 0, 0
+    while len(out) < blk * blk:
+        while y >= 0:
+            if x < blk and y < blk:
+                out.append((x, y))
+            y -= 1
+            x += 1
+        y, x = x, 0
+    return out
+
+
+def default_scaling_list(size_id, matrix_id):
+    """Table 7-5 (4x4: flat 16) / Table 7-6 (8x8 and larger: intra for matrixId 0..2, inter 3..5)."""
+    if size_id == 0:
+        return [16] * 16
+    return list(SL_DEFAULT_8X8_INTRA if matrix_id < 3 else SL_DEFAULT_8X8_INTER)
+
+
+def scaling_lists_from_syntax(sld):
+    """scaling_list_data() syntax values -> (ScalingList[sizeId][matrixId], dc[sizeId][matrixId]) (7.4.5).
+
+    ``sld``: {(size_id, matrix_id): ("pred", delta) | ("coded", dc_coef_minus8 or None, [delta_coef, ...])} for
+    sizeId 0..3, matrixId 0..5 (sizeId 3: 0 and 3, the numbering of the 2016+ editions; v1's 0 / 1 code the
+    same two lists).  Predicted lists copy refMatrixId = matrixId - delta * (sizeId == 3 ? 3 : 1), or the
+    default list (Table 7-5/7-6) and DC 16 when delta is 0."""
+    lists, dcs = {}, {}
+    for size_id in range(4):
+        for matrix_id in range(0, 6, 3 if size_id == 3 else 1):
+            kind = sld[(size_id, matrix_id)]
+            if kind[0] == "pred":
+                delta = kind[1]
+                if delta == 0:
+                    lists[(size_id, matrix_id)] = default_scaling_list(size_id, matrix_id)
+                    dcs[(size_id, matrix_id)] = 16
+                else:
+                    ref = matrix_id - delta * (3 if size_id == 3 else 1)
+                    lists[(size_id, matrix_id)] = list(lists[(size_id, ref)])
+                    dcs[(size_id, matrix_id)] = dcs.get((size_id, ref), 16)
+            else:
+                _, dc_minus8, deltas = kind
+                nxt = 8
+                if size_id > 1:
+                    nxt = dc_minus8 + 8
+                    dcs[(size_id, matrix_id)] = nxt
+                vals = []
+                for dlt in deltas:
+                    nxt = (nxt + dlt + 256) % 256
+                    vals.append(nxt)
+                lists[(size_id, matrix_id)] = vals
+    return lists, dcs
+
+
+def scaling_factors(lists, dcs):
+    """ScalingFactor (7.4.5) of the intra matrices used by 4:2:0 (sizeId 0..2: Y, Cb, Cr; sizeId 3: Y) as
+    {(size_id, matrix_id): m[y][x]} (int64 arrays; the spec's ScalingFactor[..][x][y] transposed)."""
+    out = {}
+    for (size_id, matrix_id) in SF_OFFSETS:
+        n = 4 << size_id
+        lst = lists[(size_id, matrix_id)]
+        blk = 4 if size_id == 0 else 8
+        rep = n // blk
+        m = np.zeros((n, n), np.int64)
+        for i, (x, y) in enumerate(diag_scan(blk)):
+            m[y * rep:(y + 1) * rep, x * rep:(x + 1) * rep] = lst[i]
+        if size_id > 1:
+            m[0, 0] = dcs[(size_id, matrix_id)]
+        out[(size_id, matrix_id)] = m
+    return out
+
+
+def scaling_factor_bytes(factors):
+    """{(size_id, matrix_id): m[y][x]} -> the 2032-byte ABI array (p265r_set_scaling_factors)."""
+    b = np.zeros(SF_BYTES, np.uint8)
+    for k, off in SF_OFFSETS.items():
+        m = np.asarray(factors[k])
+        b[off:off + m.size] = m.reshape(-1)
+    return b
+
+
+def factor_of(sf_bytes, log2, c_idx):
+    """m[y][x] of a TB (log2 size, component) from the 2032-byte ABI array (intra: matrixId = c_idx)."""
+    off = SF_OFFSETS[(log2 - 2, c_idx)]
+    n = 1 << log2
+    return np.asarray(sf_bytes[off:off + n * n], np.int64).reshape(n, n)
+
+
 CTU_LF_ACROSS_SLICES, CTU_DEBLOCK = 1, 2
 
 # Table 8-12: beta' (Q = 0..51) and tC' (Q = 0..53)
@@ -105,13 +213,15 @@ def transform_matrix(log2, tr_type):
 # Residual: scaling (8.6.3), transform (8.6.4.2), residual (8.6.2)
 # ---------------------------------------------------------------------------
 
-def dequantize(level, qp, log2, bit_depth):
+def dequantize(level, qp, log2, bit_depth, m=None):
     """d = Clip3(-32768, 32767, (L*m*levelScale[qP%6] << (qP/6) + (1 << (bdShift-1))) >> bdShift).
 
-    Follows decoder/scaling.py:4-47 (formula at scaling.py:45-46), m = 16 (no scaling lists).
+    Follows decoder/scaling.py:4-47 (formula at scaling.py:45-46): m = 16 without scaling lists, else the
+    TB's ScalingFactor m[y][x] (scaling.py:32-44; applied to 4x4 transform-skip blocks too, 8.6.4.2).
     """
     bd_shift = bit_depth + log2 - 5
-    v = (np.asarray(level, np.int64) * 16 * LEVEL_SCALE[qp % 6]) << (qp // 6)
+    mm = 16 if m is None else np.asarray(m, np.int64)
+    v = (np.asarray(level, np.int64) * mm * LEVEL_SCALE[qp % 6]) << (qp // 6)
     v = (v + (1 << (bd_shift - 1))) >> bd_shift
     return np.clip(v, -32768, 32767)
 
@@ -124,12 +234,13 @@ def inverse_transform(d, log2, tr_type):
     return g @ t                                    # then rows
 
 
-def residual_block(level, log2, c_idx, qp, flags, bit_depth):
-    """Residual samples r[y][x] for one TB (8.6.2).  level: N x N TransCoeffLevel [y][x]."""
+def residual_block(level, log2, c_idx, qp, flags, bit_depth, m=None):
+    """Residual samples r[y][x] for one TB (8.6.2).  level: N x N TransCoeffLevel [y][x]; m: its
+    ScalingFactor [y][x] (None: flat 16)."""
     level = np.asarray(level, np.int64)
     if flags & (TB_BYPASS | TB_PCM):
         return level.copy()
-    d = dequantize(level, qp, log2, bit_depth)
+    d = dequantize(level, qp, log2, bit_depth, m)
     if flags & TB_TSKIP:
         r = d << (5 + log2)                         # tsShift = 5 + Log2(nTbS) (= 7 for 4x4)
     else:
@@ -323,15 +434,18 @@ def reconstruct_picture(params, pic):
     planes = [np.zeros(s, np.int64) for s in _plane_shapes(params)]
     bd = [int(params["bit_depth_luma"]), int(params["bit_depth_chroma"]), int(params["bit_depth_chroma"])]
     strong = bool(params["strong_intra_smoothing"])
+    sf = params.get("scaling_factors") if int(params.get("scaling_list_enabled", 0)) else None
+    if int(params.get("scaling_list_enabled", 0)) and sf is None:
+        raise ValueError("scaling_list_enabled needs params['scaling_factors'] (scaling_factor_bytes)")
     ctus, tbs, coef = pic["ctus"], pic["tbs"], pic["coef"]
     for rs in geo.ts_order:
         c = ctus[rs]
         for t in tbs[int(c["tb_begin"]): int(c["tb_begin"]) + int(c["tb_count"])]:
-            _recon_tb(geo, planes, t, coef, bd, strong)
+            _recon_tb(geo, planes, t, coef, bd, strong, sf)
     return planes
 
 
-def _recon_tb(geo, planes, t, coef, bd, strong):
+def _recon_tb(geo, planes, t, coef, bd, strong, sf=None):
     c_idx, log2 = int(t["c_idx"]), int(t["log2_size"])
     n = 1 << log2
     x0, y0 = int(t["x"]), int(t["y"])
@@ -341,7 +455,8 @@ def _recon_tb(geo, planes, t, coef, bd, strong):
     if flags & (TB_CBF | TB_PCM):
         off = int(t["coef_off"])
         level = np.asarray(coef[off: off + n * n], np.int64).reshape(n, n)
-        res = residual_block(level, log2, c_idx, int(t["qp"]), flags, bd[c_idx])
+        m = None if sf is None else factor_of(sf, log2, c_idx)
+        res = residual_block(level, log2, c_idx, int(t["qp"]), flags, bd[c_idx], m)
     else:
         res = np.zeros((n, n), np.int64)
     if flags & TB_PCM:

@@ -19,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("P265R_LIB", os.path.join(HERE, "libp265r.so"))
 
 DIGEST_SLOTS = 64                # P265R_DIGEST_SLOTS
+SCALING_FACTOR_BYTES = 2032      # P265R_SCALING_FACTOR_BYTES
 
 # error codes (include/p265r.h)
 OK, EINVAL, ENOMEM, EHIP, EUNSUPPORTED, ERANGE, ESTATE, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
@@ -84,6 +85,7 @@ SIGNATURES = {
     "p265r_sync": (ctypes.c_int, [_vp]),
     "p265r_set_pipeline": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265r_set_row_waves": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "p265r_set_scaling_factors": (ctypes.c_int, [_vp, ctypes.c_void_p, ctypes.c_int]),
     "p265r_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "p265r_last_timings": (ctypes.c_int, [_vp, ctypes.POINTER(Timings)]),
     "p265r_timings_total": (ctypes.c_int, [_vp, ctypes.POINTER(Timings), ctypes.POINTER(ctypes.c_int)]),

@@ -29,7 +29,7 @@ from . import records as R
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("P265FE_LIB", os.path.join(HERE, "libp265fe.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK, EINVAL, ENOMEM, EUNSUPPORTED, EBITSTREAM = 0, -1, -2, -4, -8
 HASH_NONE, HASH_MD5, HASH_CRC, HASH_CHECKSUM = -1, 0, 1, 2
 FLUSH = 1
@@ -52,7 +52,8 @@ class PictureInfoC(ctypes.Structure):
                 ("crop_top", ctypes.c_uint16), ("crop_bottom", ctypes.c_uint16), ("nal_unit_type", ctypes.c_uint8),
                 ("hash_type", ctypes.c_int8), ("n_slices", ctypes.c_uint16), ("n_cus", ctypes.c_uint32),
                 ("hash", (ctypes.c_uint8 * 16) * 3), ("cvs_id", ctypes.c_int32),
-                ("max_num_reorder", ctypes.c_uint8), ("output_flag", ctypes.c_uint8), ("reserved", ctypes.c_uint16)]
+                ("max_num_reorder", ctypes.c_uint8), ("output_flag", ctypes.c_uint8), ("reserved", ctypes.c_uint16),
+                ("scaling_factors", ctypes.c_void_p)]
 
 
 _vp = ctypes.c_void_p
@@ -108,6 +109,7 @@ class DecodedPicture:
     cvs_id: int = 0             # coded video sequence (IRAP with NoRaslOutputFlag) counter
     max_num_reorder: int = 0    # sps_max_num_reorder_pics of its SPS (output bumping, C.5.2.2)
     output_flag: bool = True    # PicOutputFlag
+    scaling: Optional[np.ndarray] = None   # the 2032-byte intra ScalingFactor table (scaling_list_enabled)
 
 
 class _Owner:
@@ -224,7 +226,9 @@ def _collect(get, n, owner, validate, base=0):
                                   nal_unit_type=int(info.nal_unit_type), n_slices=int(info.n_slices),
                                   n_cus=int(info.n_cus), hash_type=int(info.hash_type), hash=hv,
                                   cvs_id=int(info.cvs_id), max_num_reorder=int(info.max_num_reorder),
-                                  output_flag=bool(info.output_flag)))
+                                  output_flag=bool(info.output_flag),
+                                  scaling=(np.ctypeslib.as_array(ctypes.cast(info.scaling_factors, ctypes.POINTER(ctypes.c_uint8)),
+                                                                 (2032,)).copy() if info.scaling_factors else None)))
     return out
 
 

@@ -378,6 +378,7 @@ void fill_info(const PictureJob& j, const PictureRecords& r, p265fe_picture_info
     out->n_cus = r.n_cus;
     std::memcpy(out->hash, j.hash, sizeof(out->hash));
     out->cvs_id = j.cvs;
+    out->scaling_factors = s.scaling_list_enabled ? j.act->scaling_factor.data() : nullptr;
     out->max_num_reorder = (uint8_t)s.max_num_reorder;
     out->output_flag = (uint8_t)(j.output ? 1 : 0);
 }

@@ -2,6 +2,8 @@
 // 7.3.7, E.2.1).  See fe_ps.h for the reference counterparts.
 #include "fe_ps.h"
 
+#include <cstring>
+
 #include <algorithm>
 
 namespace p265fe {
@@ -29,17 +31,84 @@ static void parse_ptl(BitReader& br, int max_sub_layers_minus1) {
     }
 }
 
-// scaling_list_data() (7.3.4; sld.py:63-117): parsed to move past it (scaling lists are
-// reported unsupported by the back-end)
-static void parse_scaling_list_data(BitReader& br) {
+// Table 7-6: default ScalingList of the 8x8 and larger matrices, intra (matrixId 0..2) and inter (3..5),
+// in coefficient order i (Table 7-5: the 4x4 default is flat 16); the reference's sld.py:13-33 tables
+static const uint8_t kSlIntra[64] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 16, 17, 16, 17, 18, 17, 18, 18, 17, 18, 21,
+                                     19, 20, 21, 20, 19, 21, 24, 22, 22, 24, 24, 22, 22, 24, 25, 25, 27, 30, 27, 25, 25, 29,
+                                     31, 35, 35, 31, 29, 36, 41, 44, 41, 36, 47, 54, 54, 47, 65, 70, 65, 88, 88, 115};
+static const uint8_t kSlInter[64] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 17, 18, 18, 18, 18, 18, 18, 20,
+                                     20, 20, 20, 20, 20, 20, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 28,
+                                     28, 28, 28, 28, 28, 33, 33, 33, 33, 33, 41, 41, 41, 41, 54, 54, 54, 71, 71, 91};
+
+static void default_list(int size_id, int matrix_id, ScalingLists& sl) {
+    for (int i = 0; i < 64; ++i)
+        sl.list[size_id][matrix_id][i] = size_id == 0 ? 16 : (matrix_id < 3 ? kSlIntra[i] : kSlInter[i]);
+    sl.dc[size_id][matrix_id] = 16;
+}
+
+ScalingLists default_scaling_lists() {
+    ScalingLists sl;
+    for (int size_id = 0; size_id < 4; ++size_id)
+        for (int matrix_id = 0; matrix_id < 6; ++matrix_id) default_list(size_id, matrix_id, sl);
+    return sl;
+}
+
+// 6.5.3 up-right diagonal scan position i of a blk x blk block
+static void diag_pos(int blk, int i, int& x, int& y) {
+    int k = 0;
+    for (int d = 0;; ++d)
+        for (int yy = d, xx = 0; yy >= 0; --yy, ++xx)
+            if (xx < blk && yy < blk && k++ == i) { x = xx; y = yy; return; }
+}
+
+void scaling_factors(const ScalingLists& sl, uint8_t out[2032]) {
+    static const int kOff[4][3] = {{0, 16, 32}, {48, 112, 176}, {240, 496, 752}, {1008, -1, -1}};
+    for (int size_id = 0; size_id < 4; ++size_id)
+        for (int m = 0; m < (size_id == 3 ? 1 : 3); ++m) {
+            const int n = 4 << size_id, blk = size_id == 0 ? 4 : 8, rep = n / blk;
+            uint8_t* f = out + kOff[size_id][m];
+            for (int i = 0; i < blk * blk; ++i) {
+                int x = 0, y = 0;
+                diag_pos(blk, i, x, y);
+                for (int j = 0; j < rep; ++j)
+                    for (int k = 0; k < rep; ++k) f[(y * rep + j) * n + x * rep + k] = sl.list[size_id][m][i];
+            }
+            if (size_id > 1) f[0] = sl.dc[size_id][m];
+        }
+}
+
+// scaling_list_data() (7.3.4; sld.py:63-117) resolved per 7.4.5 (the numbering of matrixId of the 2016+
+// editions: 0 and 3 for sizeId 3, refMatrixId = matrixId - delta * 3 there; v1's 0 / 1 code the same lists)
+static void parse_scaling_list_data(BitReader& br, ScalingLists& sl) {
     for (int size_id = 0; size_id < 4; ++size_id)
         for (int matrix_id = 0; matrix_id < 6; matrix_id += (size_id == 3) ? 3 : 1) {
-            if (!br.flag()) {
-                br.ue();   // scaling_list_pred_matrix_id_delta
+            if (!br.flag()) {                                      // scaling_list_pred_mode_flag = 0
+                const uint32_t delta = br.ue();                    // scaling_list_pred_matrix_id_delta
+                const int step = size_id == 3 ? 3 : 1;
+                if (delta > (uint32_t)(matrix_id / step)) bs_fail("scaling_list_pred_matrix_id_delta out of range");
+                if (delta == 0) {
+                    default_list(size_id, matrix_id, sl);
+                } else {
+                    const int ref = matrix_id - (int)delta * step;
+                    std::memcpy(sl.list[size_id][matrix_id], sl.list[size_id][ref], 64);
+                    sl.dc[size_id][matrix_id] = sl.dc[size_id][ref];
+                }
             } else {
-                int coef_num = std::min(64, 1 << (4 + (size_id << 1)));
-                if (size_id > 1) br.se();   // scaling_list_dc_coef_minus8
-                for (int i = 0; i < coef_num; ++i) br.se();
+                int next = 8;
+                const int coef_num = std::min(64, 1 << (4 + (size_id << 1)));
+                if (size_id > 1) {
+                    const int dc = br.se();                        // scaling_list_dc_coef_minus8
+                    if (dc < -7 || dc > 247) bs_fail("scaling_list_dc_coef_minus8 out of range");
+                    next = dc + 8;
+                    sl.dc[size_id][matrix_id] = (uint8_t)next;
+                }
+                for (int i = 0; i < coef_num; ++i) {
+                    const int d = br.se();                         // scaling_list_delta_coef
+                    if (d < -128 || d > 127) bs_fail("scaling_list_delta_coef out of range");
+                    next = (next + d + 256) % 256;
+                    if (next == 0) bs_fail("ScalingList value 0");
+                    sl.list[size_id][matrix_id][i] = (uint8_t)next;
+                }
             }
         }
 }
@@ -237,8 +306,10 @@ Sps parse_sps(BitReader& br) {
     if ((s.width & ((1 << s.log2_min_cb) - 1)) || (s.height & ((1 << s.log2_min_cb) - 1)))
         bs_fail("picture size not a multiple of MinCbSizeY");
     s.scaling_list_enabled = br.flag();
+    s.scaling = default_scaling_lists();
     if (s.scaling_list_enabled) {
-        if (br.flag()) parse_scaling_list_data(br);
+        s.scaling_list_data_present = br.flag();
+        if (s.scaling_list_data_present) parse_scaling_list_data(br, s.scaling);
     }
     s.amp = br.flag();
     s.sao = br.flag();
@@ -325,7 +396,8 @@ Pps parse_pps(BitReader& br) {
         }
     }
     p.scaling_list_data_present = br.flag();
-    if (p.scaling_list_data_present) parse_scaling_list_data(br);
+    p.scaling = default_scaling_lists();
+    if (p.scaling_list_data_present) parse_scaling_list_data(br, p.scaling);
     p.lists_modification_present = br.flag();
     p.log2_parallel_merge_level = 2 + (int)br.ue();
     p.slice_header_extension_present = br.flag();
@@ -399,6 +471,9 @@ std::shared_ptr<const Active> activate(const Sps& sps, const Pps& pps) {
                 for (int x = a->col_bd[i]; x < a->col_bd[i + 1]; ++x) a->tile_id_ts[a->rs_to_ts[y * W + x]] = tid;
     a->log2_min_cu_qp_delta = sps.log2_ctb - pps.diff_cu_qp_delta_depth;
     if (a->log2_min_cu_qp_delta < sps.log2_min_cb) bs_fail("diff_cu_qp_delta_depth out of range");
+    // ScalingFactor (7.4.5): the PPS lists when present, else the SPS lists (the defaults when the SPS
+    // codes none)
+    if (sps.scaling_list_enabled) scaling_factors(pps.scaling_list_data_present ? pps.scaling : sps.scaling, a->scaling_factor.data());
     return a;
 }
 

@@ -23,6 +23,16 @@ struct StRps {            // st_ref_pic_set() (7.3.7) with its derived lists (7.
     int num_delta_pocs() const { return num_negative + num_positive; }
 };
 
+// scaling_list_data() (7.3.4) resolved by 7.4.5: ScalingList[sizeId][matrixId][i] (predicted lists copied,
+// defaults of Table 7-5 / 7-6 filled in) and the 16x16 / 32x32 DC values
+struct ScalingLists {
+    uint8_t list[4][6][64] = {};
+    uint8_t dc[4][6] = {};
+};
+ScalingLists default_scaling_lists();
+// ScalingFactor (7.4.5) of the intra matrices 4:2:0 uses, in p265r_set_scaling_factors' layout (2032 B)
+void scaling_factors(const ScalingLists& sl, uint8_t out[2032]);
+
 struct Sps {
     int sps_id = 0, vps_id = 0, max_sub_layers_minus1 = 0;
     int chroma_format_idc = 1, separate_colour_plane = 0;
@@ -33,7 +43,8 @@ struct Sps {
     int max_num_reorder = 0;          // sps_max_num_reorder_pics[sps_max_sub_layers_minus1] (C.5.2.2 bumping)
     int log2_min_cb = 3, log2_ctb = 4, log2_min_tb = 2, log2_max_tb = 5;
     int max_th_depth_inter = 0, max_th_depth_intra = 0;
-    int scaling_list_enabled = 0;
+    int scaling_list_enabled = 0, scaling_list_data_present = 0;
+    ScalingLists scaling;             // sps_scaling_list_data (defaults when not present)
     int amp = 0, sao = 0;
     int pcm = 0, pcm_bit_depth_y = 8, pcm_bit_depth_c = 8, log2_min_pcm = 3, log2_max_pcm = 3, pcm_loop_filter_disabled = 0;
     std::vector<StRps> st_rps;
@@ -62,6 +73,7 @@ struct Pps {
     int deblocking_control_present = 0, deblocking_override_enabled = 0, deblocking_disabled = 0;
     int beta_offset_div2 = 0, tc_offset_div2 = 0;
     int scaling_list_data_present = 0, lists_modification_present = 0, log2_parallel_merge_level = 2;
+    ScalingLists scaling;             // pps_scaling_list_data (when present)
     int slice_header_extension_present = 0;
     int range_extension_flags = 0;   // any pps_range_extension() feature used (unsupported)
 };
@@ -75,6 +87,8 @@ struct Active {
     std::vector<int> rs_to_ts, ts_to_rs, tile_id_ts;
     std::vector<int> ctb_col_tile, ctb_row_tile;   // tile column / row of a CTB column / row
     int log2_min_cu_qp_delta = 0;
+    std::array<uint8_t, 2032> scaling_factor{};   // ScalingFactor (PPS lists, else SPS lists, else defaults)
+                                                  // when sps.scaling_list_enabled
     int tile_id_rs(int rs) const { return tile_id_ts[rs_to_ts[rs]]; }
 };
 std::shared_ptr<const Active> activate(const Sps& sps, const Pps& pps);

@@ -182,6 +182,7 @@ struct p265r_ctx {
     hipEvent_t last_intra_ev = nullptr, last_lf_ev = nullptr;
     bool last_intra_valid = false, last_lf_valid = false;
     std::string describe;             // p265r_describe text
+    uint8_t* d_sf = nullptr;           // scaling lists: the intra ScalingFactor table (p265r_set_scaling_factors)
     unsigned char* dl_stage = nullptr;  // pinned download bounce buffer, 2 x kDlHalf (first download)
     hipEvent_t dl_ev[2] = {nullptr, nullptr};
 };
@@ -504,7 +505,7 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     if (!params_ok(p)) return P265R_EINVAL;
     // BitDepth 8 (uint8_t planes, the row pipeline) or 9..10 with one depth for luma and chroma (Main 10:
     // uint16_t planes, the per-diagonal intra kernel and loopfilter16.h)
-    if (p.bit_depth_luma < 8 || p.bit_depth_luma > 10 || p.bit_depth_chroma != p.bit_depth_luma || p.scaling_list_enabled)
+    if (p.bit_depth_luma < 8 || p.bit_depth_luma > 10 || p.bit_depth_chroma != p.bit_depth_luma || p.scaling_list_enabled > 1)
         return P265R_EUNSUPPORTED;
     const int n = p265r_device_count();
     if (n < 0) return n;
@@ -621,6 +622,7 @@ void p265r_destroy(p265r_ctx* ctx) {
     if (ctx->up_stream) (void)hipStreamDestroy(ctx->up_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cache_mem) (void)hipFree(ctx->cache_mem);
+    if (ctx->d_sf) (void)hipFree(ctx->d_sf);
     if (ctx->dl_stage) (void)hipHostFree(ctx->dl_stage);
     for (hipEvent_t e : ctx->dl_ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stage) { if (ctx->stage_pinned) (void)hipHostFree(ctx->stage); else std::free(ctx->stage); }
@@ -968,6 +970,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     // loop filters) on RE-RUNS of a resident batch: its residuals / job lists from the previous
     // run are still in place, so the output is unchanged while the skipped phase costs nothing
     const int skip = b->runs > 0 ? ctx->skip : 0;
+    if (ctx->params.scaling_list_enabled && !ctx->d_sf && !b->recon_input) return P265R_ESTATE;   // factors not set
+    const uint8_t* sf = ctx->params.scaling_list_enabled ? ctx->d_sf : nullptr;
     ++b->runs;
     ctx->lane_busy |= 1u << b->lane;
     const bool prep = recon && ctx->schedule == 1 && !(skip & 2);
@@ -1052,28 +1056,31 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         return P265R_OK;
     };
     if (prep && !ctx->prep_last) { int rc = launch_prep(); if (rc) return rc; }
-    if (recon && !(skip & 1) && b->n_jobs[RC_DST4]) {
-        residual4_kernel<true><<<(b->n_jobs[RC_DST4] + 255) / 256, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
-        ++tm.residual_launches;
-    }
-    if (recon && !(skip & 1) && b->n_jobs[RC_DCT4]) {
-        residual4_kernel<false><<<(b->n_jobs[RC_DCT4] + 255) / 256, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
-        ++tm.residual_launches;
-    }
-    if (recon && !(skip & 1) && b->n_jobs[RC_DCT8]) {
-        residualN_kernel<3><<<(b->n_jobs[RC_DCT8] + 31) / 32, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
-        ++tm.residual_launches;
-    }
-    if (recon && !(skip & 1) && b->n_jobs[RC_DCT16]) {
-        residualN_kernel<4><<<(b->n_jobs[RC_DCT16] + 15) / 16, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
-        ++tm.residual_launches;
-    }
-    if (recon && !(skip & 1) && b->n_jobs[RC_DCT32]) {
-        residualN_kernel<5><<<(b->n_jobs[RC_DCT32] + 7) / 8, 256, ctx->res_lds, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
-        ++tm.residual_launches;
-    }
+    // (scaling lists: the SL instances, which read m from the context's ScalingFactor table)
+#define P265R_RES_LAUNCH(K, KSL, blocks, ...)                                                                     \
+    do {                                                                                                          \
+        if (sf) KSL<<<(blocks), 256, ctx->res_lds, rs>>>(__VA_ARGS__, sf);                                        \
+        else K<<<(blocks), 256, ctx->res_lds, rs>>>(__VA_ARGS__, nullptr);                                        \
+        ++tm.residual_launches;                                                                                   \
+    } while (0)
+    if (recon && !(skip & 1) && b->n_jobs[RC_DST4])
+        P265R_RES_LAUNCH((residual4_kernel<true, false>), (residual4_kernel<true, true>), (b->n_jobs[RC_DST4] + 255) / 256,
+                         b->d_pool, b->d_res, b->d_jobs[RC_DST4], b->n_jobs[RC_DST4], bdl, b->slab[RC_DST4]);
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT4])
+        P265R_RES_LAUNCH((residual4_kernel<false, false>), (residual4_kernel<false, true>), (b->n_jobs[RC_DCT4] + 255) / 256,
+                         b->d_pool, b->d_res, b->d_jobs[RC_DCT4], b->n_jobs[RC_DCT4], bdc, b->slab[RC_DCT4]);
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT8])
+        P265R_RES_LAUNCH((residualN_kernel<3, false>), (residualN_kernel<3, true>), (b->n_jobs[RC_DCT8] + 31) / 32,
+                         b->d_pool, b->d_res, b->d_jobs[RC_DCT8], b->n_jobs[RC_DCT8], bdl, bdc, b->slab[RC_DCT8]);
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT16])
+        P265R_RES_LAUNCH((residualN_kernel<4, false>), (residualN_kernel<4, true>), (b->n_jobs[RC_DCT16] + 15) / 16,
+                         b->d_pool, b->d_res, b->d_jobs[RC_DCT16], b->n_jobs[RC_DCT16], bdl, bdc, b->slab[RC_DCT16]);
+    if (recon && !(skip & 1) && b->n_jobs[RC_DCT32])
+        P265R_RES_LAUNCH((residualN_kernel<5, false>), (residualN_kernel<5, true>), (b->n_jobs[RC_DCT32] + 7) / 8,
+                         b->d_pool, b->d_res, b->d_jobs[RC_DCT32], b->n_jobs[RC_DCT32], bdl, bdc, b->slab[RC_DCT32]);
+#undef P265R_RES_LAUNCH
     if (recon && !(skip & 1) && b->n_jobs[RC_TSKIP]) {
-        residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc);
+        residual_tskip_kernel<<<(b->n_jobs[RC_TSKIP] + 255) / 256, 256, 0, rs>>>(b->d_pool, b->d_res, b->d_jobs[RC_TSKIP], b->n_jobs[RC_TSKIP], bdl, bdc, sf);
         ++tm.residual_launches;
     }
     if (prep && ctx->prep_last) { int rc = launch_prep(); if (rc) return rc; }
@@ -1492,6 +1499,18 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         buf[k] = 0;
     }
     return n;
+}
+
+int p265r_set_scaling_factors(p265r_ctx* ctx, const uint8_t* factors, int n_bytes) {
+    if (!ctx || !factors || n_bytes != P265R_SCALING_FACTOR_BYTES) return P265R_EINVAL;
+    if (!ctx->params.scaling_list_enabled) return P265R_ESTATE;
+    for (int i = 0; i < n_bytes; ++i)
+        if (factors[i] == 0) return P265R_EINVAL;              // ScalingFactor is 1..255 (7.4.5)
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = p265r_sync(ctx)) return rc;                    // no run in flight reads the old table
+    if (!ctx->d_sf) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ctx->d_sf), P265R_SCALING_FACTOR_BYTES));
+    HIP_TRY(hipMemcpy(ctx->d_sf, factors, P265R_SCALING_FACTOR_BYTES, hipMemcpyHostToDevice));
+    return P265R_OK;
 }
 
 int p265r_set_row_waves(p265r_ctx* ctx, int waves) {

@@ -65,6 +65,26 @@ struct Dequant {
     }
 };
 
+// Scaling lists (scaling_list_enabled_flag; decoder/scaling.py:32-44): m[y][x] = the TB's ScalingFactor
+// instead of 16, from the context's 2032-byte table (p265r_set_scaling_factors: intra matrices, [y][x] per
+// (sizeId, matrixId = cIdx)).  |L * m * levelScale| < 2^31, but the << qP / 6 needs 64 bits.
+__host__ __device__ __forceinline__ int sf_offset(int log2, int c_idx) {
+    // 4x4 Y/Cb/Cr at 0/16/32, 8x8 at 48/112/176, 16x16 at 240/496/752, 32x32 Y at 1008
+    return log2 == 2 ? 16 * c_idx : (log2 == 3 ? 48 + 64 * c_idx : (log2 == 4 ? 240 + 256 * c_idx : 1008));
+}
+struct DequantM {
+    int ls, per, bds;
+    __device__ __forceinline__ DequantM(int qp, int bd_shift) {
+        per = qp / 6;
+        ls = (int)((0x484039332D28ull >> (8 * (qp - 6 * per))) & 0xffu);
+        bds = bd_shift;
+    }
+    __device__ __forceinline__ int operator()(int level, int m) const {
+        const long long v = (long long)(level * m * ls) << per;
+        return clamp16((v + (1ll << (bds - 1))) >> bds);
+    }
+};
+
 // ---------------------------------------------------------------------------
 // 4x4: one thread per TB, everything in registers.
 // ---------------------------------------------------------------------------
@@ -92,11 +112,11 @@ __device__ __forceinline__ void inv4(const int (&c)[4], int (&o)[4]) {
 // A class's TBs are packed back to back in job order (p265r_batch_upload), so TB i of a fixed-size
 // class sits at slab + i * N * N: the coefficient loads do not wait for the job record (which
 // only supplies qP), one dependent memory round trip less per TB.
-template <bool DST>
+template <bool DST, bool SL = false>
 __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restrict__ pool,
                                                         int16_t* __restrict__ res,
                                                         const ResJob* __restrict__ jobs, int n_jobs,
-                                                        int bit_depth, uint32_t slab) {
+                                                        int bit_depth, uint32_t slab, const uint8_t* __restrict__ sf) {
     P265R_BW_PRIO_SET();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_jobs) return;
@@ -107,12 +127,23 @@ __global__ __launch_bounds__(256) void residual4_kernel(const int16_t* __restric
     const uint4 raw0 = *reinterpret_cast<const uint4*>(blk);       // 16 x int16 = 32 B
     const uint4 raw1 = *reinterpret_cast<const uint4*>(blk + 8);
     const uint32_t w[8] = {raw0.x, raw0.y, raw0.z, raw0.w, raw1.x, raw1.y, raw1.z, raw1.w};
-    const Dequant dq(jb.qp, bit_depth + 2 - 5);
     int d[4][4];
+    if constexpr (SL) {
+        const DequantM dq(jb.qp, bit_depth + 2 - 5);
+        const uint4 mw = *reinterpret_cast<const uint4*>(sf + sf_offset(2, jb.c_idx));
+        const uint32_t mv[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int lv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffff);
-        d[k >> 2][k & 3] = dq(lv);
+        for (int k = 0; k < 16; ++k) {
+            const int lv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffff);
+            d[k >> 2][k & 3] = dq(lv, (int)((mv[k >> 2] >> (8 * (k & 3))) & 0xffu));
+        }
+    } else {
+        const Dequant dq(jb.qp, bit_depth + 2 - 5);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int lv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffff);
+            d[k >> 2][k & 3] = dq(lv);
+        }
     }
     int g[4][4];
 #pragma unroll
@@ -232,11 +263,12 @@ __device__ __forceinline__ void inv_dct_d2(const int (&c)[N], int (&x)[N], int r
 //   thread r: row transform (stage 2) + bdShift -> 16-B vector stores, in place.
 // Matrix entries are compile-time immediates (fully unrolled).
 // ---------------------------------------------------------------------------
-template <int LOG2>
+template <int LOG2, bool SL = false>
 __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restrict__ pool,
                                                        int16_t* __restrict__ res,
                                                        const ResJob* __restrict__ jobs, int n_jobs,
-                                                       int bit_depth_luma, int bit_depth_chroma, uint32_t slab) {
+                                                       int bit_depth_luma, int bit_depth_chroma, uint32_t slab,
+                                                       const uint8_t* __restrict__ sf) {
     P265R_BW_PRIO_SET();
     constexpr int N = 1 << LOG2;
     constexpr int TPB = 256 / N;                 // TBs per block
@@ -252,7 +284,22 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
     const int16_t* blk = pool + off;
     int16_t* dst = res + off;
     const int bit_depth = jb.c_idx ? bit_depth_chroma : bit_depth_luma;
-    if (active) {
+    if (active && SL) {
+        const DequantM dq(jb.qp, bit_depth + LOG2 - 5);
+        const uint8_t* mrow = sf + sf_offset(LOG2, jb.c_idx) + lane * N;      // m[row = lane][..]
+#pragma unroll
+        for (int v = 0; v < N / 8; ++v) {
+            const uint4 raw = *reinterpret_cast<const uint4*>(blk + lane * N + v * 8);
+            const uint2 mw = *reinterpret_cast<const uint2*>(mrow + v * 8);
+            const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int lv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xffff);
+                const int m = (int)((((k < 4) ? mw.x : mw.y) >> (8 * (k & 3))) & 0xffu);
+                t[lane * S + v * 8 + k] = (int16_t)dq(lv, m);
+            }
+        }
+    } else if (active) {
         const Dequant dq(jb.qp, bit_depth + LOG2 - 5);
 #pragma unroll
         for (int v = 0; v < N / 8; ++v) {
@@ -326,19 +373,22 @@ __global__ __launch_bounds__(256) void residualN_kernel(const int16_t* __restric
 __global__ __launch_bounds__(256) void residual_tskip_kernel(const int16_t* __restrict__ pool,
                                                              int16_t* __restrict__ res,
                                                              const ResJob* __restrict__ jobs, int n_jobs,
-                                                             int bit_depth_luma, int bit_depth_chroma) {
+                                                             int bit_depth_luma, int bit_depth_chroma,
+                                                             const uint8_t* __restrict__ sf) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_jobs) return;
     const ResJob jb = jobs[i];
     const int bd = jb.c_idx ? bit_depth_chroma : bit_depth_luma;
     const Dequant dq(jb.qp, bd + jb.log2 - 5);
+    const DequantM dqm(jb.qp, bd + jb.log2 - 5);        // scaling lists: m applies to transform skip too (8.6.4.2)
+    const uint8_t* m = sf ? sf + sf_offset(jb.log2, jb.c_idx) : nullptr;
     const int ts = 5 + jb.log2;
     const int bd2 = 20 - bd;
     const int n2 = 1 << (2 * jb.log2);
     const int16_t* blk = pool + jb.off;
     int16_t* dst = res + jb.off;
     for (int k = 0; k < n2; ++k) {
-        const long long r = (long long)dq(blk[k]) << ts;
+        const long long r = (long long)(m ? dqm(blk[k], m[k]) : dq(blk[k])) << ts;
         dst[k] = (int16_t)clamp16((r + (1 << (bd2 - 1))) >> bd2);
     }
 }

@@ -100,13 +100,18 @@ _CONTEXT_CACHE = {}                    # key -> [idle ReconContext]
 _CONTEXT_LOCK = threading.Lock()
 
 
-def _context(params, device, pipeline):
-    key = (int(device), params.tobytes(), int(pipeline))
+def _param_key(params, scaling):
+    """A picture's back-end configuration: its params POD and, with scaling lists, its ScalingFactor table."""
+    return params.tobytes() + (b"" if scaling is None else np.asarray(scaling, np.uint8).tobytes())
+
+
+def _context(params, device, pipeline, scaling=None):
+    key = (int(device), _param_key(params, scaling), int(pipeline))
     with _CONTEXT_LOCK:
         idle = _CONTEXT_CACHE.get(key)
         ctx = idle.pop() if idle else None         # checked out: one user at a time
     if ctx is None:
-        ctx = recon.ReconContext(params, device=device)
+        ctx = recon.ReconContext(params, device=device, scaling=scaling)
         ctx.set_pipeline(max(1, min(16, pipeline)))
     return key, ctx
 
@@ -217,17 +222,17 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT
     lanes = {}                          # params bytes -> [_Lane] * depth
     k_submit = [0]
 
-    def lanes_for(params):
-        key = params.tobytes()
+    def lanes_for(params, scaling):
+        key = _param_key(params, scaling)
         ls = lanes.get(key)
         if ls is None:
             t0 = clock()
-            ls = lanes[key] = [_Lane(*_context(params, device, 1)) for _ in range(depth)]
+            ls = lanes[key] = [_Lane(*_context(params, device, 1, scaling)) for _ in range(depth)]
             st.add("context", clock() - t0)
         return ls
 
     def submit(group):
-        lane = lanes_for(group[0].params)[k_submit[0] % depth]
+        lane = lanes_for(group[0].params, group[0].scaling)[k_submit[0] % depth]
         k_submit[0] += 1
         slots.acquire()                 # at most `depth` batches between upload and download
         if stop.is_set():
@@ -253,7 +258,8 @@ def decode_chunks(chunks: Iterable[bytes], device: int = 0, batch: int = DEFAULT
                     raise item
                 end = item is None
                 for d in item or []:
-                    if pending and (len(pending) >= batch or d.params.tobytes() != pending[0].params.tobytes()):
+                    if pending and (len(pending) >= batch or
+                                    _param_key(d.params, d.scaling) != _param_key(pending[0].params, pending[0].scaling)):
                         submit(pending)
                         pending = []
                     pending.append(d)

@@ -80,7 +80,9 @@ class Batch:
 class ReconContext:
     """One HIP device + stream + parameter set (p265r_ctx)."""
 
-    def __init__(self, params, device=0):
+    def __init__(self, params, device=0, scaling=None):
+        """``scaling``: the 2032-byte intra ScalingFactor table (p265r_set_scaling_factors) when
+        params.scaling_list_enabled."""
         self.lib = _lib.load()
         self.params = params
         self._pc = _params_c(params)
@@ -88,6 +90,14 @@ class ReconContext:
         _lib.check(self.lib.p265r_create(device, ctypes.byref(self._pc), ctypes.byref(h)), "p265r_create")
         self.handle = h
         self.device = device
+        if scaling is not None:
+            self.set_scaling_factors(scaling)
+
+    def set_scaling_factors(self, factors):
+        """The intra ScalingFactor table (2032 bytes, include/p265r.h) for every later run."""
+        f = np.ascontiguousarray(factors, np.uint8).reshape(-1)
+        _lib.check(self.lib.p265r_set_scaling_factors(self.handle, f.ctypes.data, int(f.size)),
+                   "p265r_set_scaling_factors")
 
     def close(self):
         if getattr(self, "handle", None):

@@ -30,6 +30,7 @@ intra.py:160 edge-filter clip), samples 0..1023 and QpY -12..51.  The 8-bit run 
 """
 import contextlib
 import hashlib
+import importlib
 import io
 import json
 import os
@@ -208,8 +209,71 @@ def main(bd=8):
     print(json.dumps(meta, indent=1))
 
 
+def main_scaling():
+    """--scaling: the ScalingFactor branch of scaling.inverse_scaling (scaling.py:32-44, m[x][y] =
+    sps.scaling_factor[size_id][matrix_id][x][y]) on seeded random factors (1..255) and levels, 8 and 10
+    bits, every size and intra component; and the default scaling lists of sld.py (Table 7-5 / 7-6, data).
+    Writes ref_scaling.npz / .json."""
+    mods = _refshim.install("/tmp/p265_component_fixture")
+    _refshim.silence(mods)
+    intra, scaling, sld = mods["intra"], mods["scaling"], importlib.import_module("sld")
+    rng = np.random.default_rng(SEED + 1)
+    cases = dict(n=[], qp=[], c=[], bd=[], level=[], m=[], out=[])
+    for case in range(200):
+        n = [4, 8, 16, 32][case % 4]
+        log2 = int(np.log2(n))
+        c_idx = 0 if n == 32 else int(rng.integers(0, 3))
+        bd = 8 if case % 2 == 0 else 10
+        off = 6 * (bd - 8)
+        qp = int(rng.integers(-off, 52))
+        sf = np.zeros((4, 6, 32, 32), np.int64)
+        mx = rng.integers(1, 256, (n, n))                 # [x][y] as the reference indexes it
+        sf[log2 - 2][c_idx][:n, :n] = mx
+        sps = _NS(bit_depth_y=bd, bit_depth_c=bd, qp_bd_offset_y=off, qp_bd_offset_c=off,
+                  scaling_list_enabled_flag=1, scaling_factor=sf)
+        lvl = np.zeros((n, n), np.int64)
+        mask = rng.random((n, n)) < 0.4
+        mag = rng.geometric(0.2, (n, n)) if case % 5 else rng.integers(1, 32768, (n, n))
+        lvl[mask] = (mag * rng.choice([-1, 1], (n, n)))[mask]
+        lvl = np.clip(lvl, -32768, 32767)
+        tu = _NS(get_trans_coeff_level=lambda x, y, c: int(lvl[y, x]))
+        cu = _NS(ctx=_NS(sps=sps), tu=tu, qp_y=qp, qp_cb=qp, qp_cr=qp, cu_transquant_bypass_flag=0,
+                 is_intra_mode=lambda: True)
+        pu = intra.IntraPu(cu, c_idx, 0, log2, 0, 0)
+        scaling.inverse_scaling(pu=pu, x0=0, y0=0, log2size=log2)
+        out = np.zeros((32, 32), np.int16)
+        out[:n, :n] = np.asarray(pu.scaled_samples).T
+        pad = np.zeros((32, 32), np.int64)
+        pad[:n, :n] = lvl
+        mpad = np.zeros((32, 32), np.uint8)
+        mpad[:n, :n] = mx.T                               # stored [y][x]
+        for k, v in (("n", n), ("qp", qp + off), ("c", c_idx), ("bd", bd), ("level", pad.astype(np.int16)),
+                     ("m", mpad), ("out", out)):
+            cases[k].append(v)
+    d = sld.ScalingListData
+    out = os.path.join(HERE, "ref_scaling.npz")
+    np.savez_compressed(out, n=np.array(cases["n"], np.uint8), qp=np.array(cases["qp"], np.uint8),
+                        c=np.array(cases["c"], np.uint8), bd=np.array(cases["bd"], np.uint8),
+                        level=np.array(cases["level"]), m=np.array(cases["m"]), out=np.array(cases["out"]),
+                        default_4x4=np.array(d.default_scaling_list_4x4, np.uint8),
+                        default_8x8_intra=np.array(d.default_scaling_list_8x8_intra, np.uint8),
+                        default_8x8_inter=np.array(d.default_scaling_list_8x8_inter, np.uint8))
+    meta = dict(generator="tests/golden/gen_component_fixture.py --scaling", seed=SEED + 1, cases=len(cases["n"]),
+                functions=["scaling.py:4-47 (ScalingFactor branch, scaling.py:32-44)",
+                           "sld.py:4-33 default_scaling_list_* (Table 7-5 / 7-6)"],
+                npz_sha256=hashlib.sha256(open(out, "rb").read()).hexdigest())
+    with open(os.path.join(HERE, "ref_scaling.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1))
+
+
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 10))
-    main(ap.parse_args().bit_depth)
+    ap.add_argument("--scaling", action="store_true", help="the ScalingFactor vectors (ref_scaling.npz) instead")
+    args = ap.parse_args()
+    if args.scaling:
+        main_scaling()
+    else:
+        main(args.bit_depth)

@@ -265,6 +265,8 @@ DEFAULTS = dict(
     split_prob=0.55, tf_split_prob=0.5, nxn_prob=0.4, cbf_prob=0.7, chroma_cbf_prob=0.35, pcm_prob=0.08,
     bypass_prob=0.1, tskip_prob=0.3, density=0.25, big_prob=0.03,
     bit_depth=8,                # BitDepthY = BitDepthC (8, or 9..10: Main 10 -- QpBdOffset, SAO cMax, PCM depths)
+    scaling_lists=None,         # None | "default" (enabled, no lists coded) | "sps" (random lists in the SPS) |
+                                # "pps" (SPS lists overridden by random PPS lists)
 )
 
 
@@ -290,6 +292,16 @@ class StreamGen:
         self.bd = c["bit_depth"]
         self.qp_off = 6 * (self.bd - 8)                  # QpBdOffsetY = QpBdOffsetC
         self.pcm_bd = (8, 7) if self.bd == 8 else (self.bd - 1, self.bd - 2)
+        self.params["scaling_list_enabled"] = int(c["scaling_lists"] is not None)
+        self.scaling_factors = None
+        if c["scaling_lists"] is not None:
+            # the syntax of both lists is drawn now (a separate stream: the picture syntax stays as it was)
+            srng = np.random.default_rng(seed + 7919)
+            self.sps_sld = self._random_sld(srng) if c["scaling_lists"] in ("sps", "pps") else None
+            self.pps_sld = self._random_sld(srng) if c["scaling_lists"] == "pps" else None
+            from oracle import recon_oracle as O
+            sld = self.pps_sld or self.sps_sld or {(s, m): ("pred", 0) for s in range(4) for m in range(0, 6, 3 if s == 3 else 1)}
+            self.scaling_factors = O.scaling_factor_bytes(O.scaling_factors(*O.scaling_lists_from_syntax(sld)))
 
     # tile structure (6.5.1)
     def _tiles(self):
@@ -324,6 +336,47 @@ class StreamGen:
 
     def tile_row0(self, cy):
         return max(b for b in self.rowbd[:-1] if b <= cy)
+
+    # ----------------------------------------------------------------- scaling lists (7.3.4)
+    @staticmethod
+    def _random_sld(r):
+        """Random scaling_list_data syntax: {(sizeId, matrixId): ("pred", delta) | ("coded", dc_minus8, deltas)},
+        every resulting list value in 1..255 (oracle.recon_oracle.scaling_lists_from_syntax's form)."""
+        sld = {}
+        for size_id in range(4):
+            step = 3 if size_id == 3 else 1
+            for matrix_id in range(0, 6, step):
+                if r.random() < 0.3:
+                    sld[(size_id, matrix_id)] = ("pred", int(r.integers(0, matrix_id // step + 1)))
+                    continue
+                n = min(64, 1 << (4 + 2 * size_id))
+                vals = r.integers(1, 256, n) if r.random() < 0.5 else np.clip(16 + np.cumsum(r.integers(-3, 6, n)), 1, 255)
+                prev, dc = 8, None
+                if size_id > 1:
+                    dcv = int(r.integers(1, 256))
+                    dc, prev = dcv - 8, dcv
+                deltas = []
+                for v in vals:
+                    d = ((int(v) - prev + 128) % 256) - 128
+                    deltas.append(d)
+                    prev = int(v)
+                sld[(size_id, matrix_id)] = ("coded", dc, deltas)
+        return sld
+
+    @staticmethod
+    def _write_sld(bw, sld):
+        for size_id in range(4):
+            for matrix_id in range(0, 6, 3 if size_id == 3 else 1):
+                kind = sld[(size_id, matrix_id)]
+                if kind[0] == "pred":
+                    bw.u(0, 1)
+                    bw.ue(kind[1])
+                else:
+                    bw.u(1, 1)
+                    if size_id > 1:
+                        bw.se(kind[1])
+                    for d in kind[2]:
+                        bw.se(d)
 
     # ----------------------------------------------------------------- parameter sets
     def vps(self):
@@ -362,7 +415,13 @@ class StreamGen:
         bw.ue(c["min_cb_log2"] - 3); bw.ue(c["ctb_log2"] - c["min_cb_log2"])
         bw.ue(c["min_tb_log2"] - 2); bw.ue(c["max_tb_log2"] - c["min_tb_log2"])
         bw.ue(c["max_th_depth"]); bw.ue(c["max_th_depth"])
-        bw.u(0, 1)                                       # scaling lists off
+        if c["scaling_lists"] is None:
+            bw.u(0, 1)                                   # scaling_list_enabled_flag 0
+        else:
+            bw.u(1, 1)
+            bw.u(int(self.sps_sld is not None), 1)       # sps_scaling_list_data_present_flag
+            if self.sps_sld is not None:
+                self._write_sld(bw, self.sps_sld)
         bw.u(1, 1); bw.u(int(c["sao"]), 1)               # amp, sao
         if c["pcm"]:
             lo, hi, lfd = c["pcm"]
@@ -423,7 +482,11 @@ class StreamGen:
             bw.u(int(dbk == "off"), 1)
             if dbk != "off":
                 bw.se(1); bw.se(-2)
-        bw.u(0, 1); bw.u(0, 1); bw.ue(0); bw.u(0, 1); bw.u(0, 1)
+        pps_sld = getattr(self, "pps_sld", None)
+        bw.u(int(pps_sld is not None), 1)               # pps_scaling_list_data_present_flag
+        if pps_sld is not None:
+            self._write_sld(bw, pps_sld)
+        bw.u(0, 1); bw.ue(0); bw.u(0, 1); bw.u(0, 1)
         bw.trailing()
         return nal(34, bw.bytes())
 
@@ -450,7 +513,8 @@ class StreamGen:
             out += nals
             if c["hash_sei"] and planes_fn is not None:
                 kind = {"md5": 0, "crc": 1, "checksum": 2}[c["hash_sei"]]
-                hv = picture_hash(planes_fn(self.params, pic), c["hash_sei"])
+                extra = {} if self.scaling_factors is None else {"scaling": self.scaling_factors}
+                hv = picture_hash(planes_fn(self.params, pic, **extra), c["hash_sei"])
                 self.last_hash = (kind, hv)
                 out.append(sei_nal(bytes([kind]) + b"".join(hv)))
             elif c["hash_sei"]:

@@ -87,9 +87,9 @@ def test_front_end_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
         assert n in bitstream.SIGNATURES, n
-    assert lib.p265fe_abi_version() == 3
-    # p265fe_picture_info layout: 32 B params + pointers/counters + 48 B hash
-    assert ctypes.sizeof(bitstream.PictureInfoC) == 160
+    assert lib.p265fe_abi_version() == 4
+    # p265fe_picture_info layout: 32 B params + pointers/counters + 48 B hash + the scaling factor pointer
+    assert ctypes.sizeof(bitstream.PictureInfoC) == 168
     h = ctypes.c_void_p()
     assert lib.p265fe_create(ctypes.byref(h)) == 0
     assert lib.p265fe_picture(h, 0, None) == bitstream.EINVAL

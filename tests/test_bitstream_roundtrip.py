@@ -44,6 +44,10 @@ CASES = {
     "main10_tiles_wpp_bypass": dict(bit_depth=10, tiles=(2, 2), wpp=True, bypass=True, qp_delta_depth=0),
     "main9_chroma_offsets": dict(bit_depth=9, slice_chroma_offsets=(3, -5), cb_qp_offset=-4, cr_qp_offset=6,
                                  qp_delta_depth=1, deblocking="override", slices=[(0, False), (20, False)]),
+    # scaling lists (7.3.4): enabled with the default lists, random lists in the SPS, SPS lists overridden by the PPS
+    "scaling_default": dict(scaling_lists="default"),
+    "scaling_sps": dict(scaling_lists="sps", tskip=True),
+    "scaling_pps_main10": dict(scaling_lists="pps", bit_depth=10, ctb_log2=5, width=160, height=96),
 }
 
 
@@ -58,6 +62,10 @@ def roundtrip(seed, threads=2, **cfg):
         assert np.array_equal(d.picture.ctus, p.ctus)
         assert np.array_equal(d.picture.tbs, p.tbs)
         assert np.array_equal(d.picture.coef, p.coef)
+        if g.scaling_factors is None:
+            assert d.scaling is None
+        else:
+            assert np.array_equal(d.scaling, g.scaling_factors)
         if p.nofilter is None:
             assert d.picture.nofilter is None
         else:
@@ -128,3 +136,35 @@ def test_hash_of_16bit_planes_matches_the_encoder(kind):
     want = streamgen.picture_hash(planes, kind)
     code = {"md5": B.HASH_MD5, "crc": B.HASH_CRC, "checksum": B.HASH_CHECKSUM}[kind]
     assert [B.plane_hash(p, code) for p in planes] == want
+
+
+@pytest.mark.parametrize("kind", ["default", "sps", "pps"])
+def test_scaling_factors_from_the_front_end(kind):
+    """The front-end's ScalingFactor table (fe_ps.cpp, 7.4.5) equals the oracle's derivation from the
+    same scaling_list_data syntax (oracle/recon_oracle.py scaling_lists_from_syntax / scaling_factors)."""
+    from oracle import recon_oracle as O
+    g, dec = roundtrip(31 + len(kind), scaling_lists=kind)
+    sf = dec[0].scaling
+    assert sf.dtype == np.uint8 and sf.size == O.SF_BYTES and sf.min() >= 1
+    if kind == "default":
+        assert (O.factor_of(sf, 2, 0) == 16).all() and O.factor_of(sf, 3, 0)[7, 7] == 115
+    else:
+        sld = g.pps_sld if kind == "pps" else g.sps_sld
+        lists, dcs = O.scaling_lists_from_syntax(sld)
+        for (size_id, m), dc in dcs.items():
+            if size_id >= 2 and (size_id, m) in O.SF_OFFSETS:   # DC: 16x16 / 32x32 intra matrices
+                assert O.factor_of(sf, size_id + 2, m)[0, 0] == dc
+        want = O.scaling_factor_bytes(O.scaling_factors(lists, dcs))
+        assert np.array_equal(sf, want)
+
+
+def test_scaling_list_syntax_errors_are_rejected():
+    """A coded list value of 0 (7.4.5: nextCoef > 0) and a refMatrixId below 0 are stream errors."""
+    g = streamgen.StreamGen(5, scaling_lists="sps")
+    g.sps_sld[(0, 0)] = ("coded", None, [-8] + [0] * 15)
+    with pytest.raises(bitstream.BitstreamError):
+        bitstream.decode_stream(g.stream()[0])
+    g = streamgen.StreamGen(5, scaling_lists="sps")
+    g.sps_sld[(1, 1)] = ("pred", 2)
+    with pytest.raises(bitstream.BitstreamError):
+        bitstream.decode_stream(g.stream()[0])

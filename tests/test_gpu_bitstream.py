@@ -28,8 +28,8 @@ def dec_mod():
     return decoder
 
 
-def oracle_planes(params, pic):
-    return c_oracle.decode(params, [pic], with_recon=False)[0][1]
+def oracle_planes(params, pic, scaling=None):
+    return c_oracle.decode(params, [pic], with_recon=False, scaling=scaling)[0][1]
 
 
 def test_sanity_bin_end_to_end(dec_mod):
@@ -57,6 +57,11 @@ CASES = {
     "main10": dict(bit_depth=10, pcm=(3, 4, True), bypass=True, qp_delta_depth=1, init_qp=14, slice_qp_delta=-18,
                    deblocking="override", slices=[(0, False), (20, False)]),
     "main10_tiles_wpp_ctb32": dict(bit_depth=10, tiles=(2, 2), wpp=True, ctb_log2=5, width=192, height=128),
+    # scaling lists: the front-end's ScalingFactor table (SPS lists, PPS override, defaults) into the residual kernels
+    "scaling_sps_tskip": dict(scaling_lists="sps", tskip=True, qp_delta_depth=1),
+    "scaling_pps_main10": dict(scaling_lists="pps", bit_depth=10, ctb_log2=5, width=160, height=96, frames=2),
+    "scaling_default_tiles": dict(scaling_lists="default", tiles=(2, 2), deblocking="override",
+                                  slices=[(0, False), (20, False)]),
 }
 
 
@@ -71,7 +76,7 @@ def test_generated_streams_match_their_picture_hash(dec_mod, name, kind):
     for f in frames:
         prm, pic, poc = pics[f.decode_index]
         assert f.poc == poc
-        want = oracle_planes(prm, pic)
+        want = oracle_planes(prm, pic, scaling=g.scaling_factors)
         for c in range(3):
             np.testing.assert_array_equal(f.planes[c], want[c])
 
