@@ -12,13 +12,21 @@ FESRC := $(wildcard p265_amd/csrc/fe/*.cpp)
 FEHDR := $(wildcard p265_amd/csrc/fe/*.h) include/p265fe.h include/p265r.h
 
 # negative-test builds of the half-CTU publish self-checks (tests/test_a_multirank.py): prep places the
-# publish point one job early, with (1) and without (2) prep's own check
-CHECKVARIANTS := p265_amd/libp265r_brbroken1.so p265_amd/libp265r_brbroken2.so
+# publish point one job early, with (1) and without (2) prep's own check; and the two A/B phase schedules
+# of a pipelined context (tests/test_gpu_parity.py, per-run digests)
+CHECKVARIANTS := p265_amd/libp265r_brbroken1.so p265_amd/libp265r_brbroken2.so \
+                 p265_amd/libp265r_phaseorder.so p265_amd/libp265r_earlyres.so
 
 all: p265_amd/libp265r.so p265_amd/libp265fe.so p265_amd/libp265probe.so $(CHECKVARIANTS) oracle
 
 p265_amd/libp265r_brbroken%.so: $(SRC) $(HDR)
 	$(HIPCC) $(HIPFLAGS) -DP265R_BR_BROKEN=$* -o $@ $(SRC)
+
+p265_amd/libp265r_phaseorder.so: $(SRC) $(HDR)
+	$(HIPCC) $(HIPFLAGS) -DP265R_PHASE_ORDER=1 -o $@ $(SRC)
+
+p265_amd/libp265r_earlyres.so: $(SRC) $(HDR)
+	$(HIPCC) $(HIPFLAGS) -DP265R_EARLY_RESIDUAL=1 -o $@ $(SRC)
 
 # measurement helper (not the product path): the row kernel's job-loop issue ceiling (bench.py)
 p265_amd/libp265probe.so: p265_amd/csrc/issue_probe.hip

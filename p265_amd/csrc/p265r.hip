@@ -1469,7 +1469,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
         "\"fair\": %d, \"quad\": %d, \"luma_lead\": %d, \"sao_rows\": %d, \"skip\": %d, \"debug_sync\": %d, "
         "\"pipeline\": %d, \"fork_prep\": %d, \"pipe_waves\": %d, \"hw_queues\": \"%s\", \"num_cus\": %d, \"diag_build\": %d, "
         "\"experiments_build\": %d, \"split\": %d, \"last_launch_split\": %d, \"xg\": %d, \"last_launch_xg\": %d, "
-        "\"phase_order\": %d, \"bit_depth\": %d, \"row_launches\": {\"w12\": %lld, \"w8\": %lld, \"w16_split\": %lld, \"xg\": %lld, \"other\": %lld}, "
+        "\"phase_order\": %d, \"early_residual\": %d, \"bit_depth\": %d, \"row_launches\": {\"w12\": %lld, \"w8\": %lld, \"w16_split\": %lld, \"xg\": %lld, \"other\": %lld}, "
         "\"env_overrides\": [%s]}",
         ctx->schedule ? "rows" : "steps", ctx->row_waves,
         ctx->row_waves ? "fixed" : (P265R_PHASE_ORDER
@@ -1489,7 +1489,7 @@ int p265r_describe(p265r_ctx* ctx, char* buf, int size) {
 #else
         0,
 #endif
-        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, ctx->xg, ctx->last_xg ? 1 : 0, P265R_PHASE_ORDER,
+        P265R_EXPERIMENTS, ctx->split, ctx->last_split ? 1 : 0, ctx->xg, ctx->last_xg ? 1 : 0, P265R_PHASE_ORDER, P265R_EARLY_RESIDUAL,
         (int)ctx->params.bit_depth_luma, ctx->row_launches[0], ctx->row_launches[1], ctx->row_launches[2], ctx->row_launches[3], ctx->row_launches[4],
         ctx->describe.c_str());
     if (n < 0) return P265R_EINVAL;

@@ -274,32 +274,62 @@ def test_pipelined_chip_filling_batches(recon_mod):
             b.free()
 
 
-def test_pipelined_chip_filling_and_small_batches_mixed(recon_mod):
+PHASE_BUILDS = {"default": None, "phase_order": "libp265r_phaseorder.so", "early_residual": "libp265r_earlyres.so"}
+
+
+@pytest.mark.parametrize("build", sorted(PHASE_BUILDS))
+def test_pipelined_chip_filling_and_small_batches_mixed(recon_mod, build):
     """One pipelined context runs a chip-filling batch (forked prep stream) interleaved with a small
     batch (all phases on its lane): every run of either must wait for its OWN previous intra phase
-    before overwriting its residual pool and job lists (with P265R_PHASE_ORDER builds the residual +
-    prep phase waits for the last intra launch of ANY lane, which a small batch's runs do not order).  Every picture of both batches is checked through
-    the device digest (p265r_batch_digest)."""
-    from p265_amd import digest
+    before overwriting its residual pool and job lists.  Every run is checked: a device digest is
+    enqueued after each one (p265r_batch_digest_async, its own slot), so a run corrupted by the next
+    run's residual phase is caught even though the next run rewrites the planes.  The A/B phase
+    schedules -- P265R_PHASE_ORDER=1 (residual + prep wait for the last intra launch of ANY lane, which a
+    small batch's runs do not order) and P265R_EARLY_RESIDUAL=1 (re-runs start their residual phase when
+    the batch's previous intra phase ends) -- run the same body in a child process on their builds."""
+    import json
+    import subprocess
+    import sys
+    if PHASE_BUILDS[build] is not None:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        lib = os.path.join(root, "p265_amd", PHASE_BUILDS[build])
+        assert os.path.exists(lib), "build the check variants first (make)"
+        env = {k: v for k, v in os.environ.items() if not k.startswith("P265R_")}
+        env.update(P265R_LIB=lib, P265R_EXPECT_BUILD=build)
+        p = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                            os.path.abspath(__file__) + "::test_pipelined_chip_filling_and_small_batches_mixed[default]"],
+                           env=env, cwd=root, capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0 and "1 passed" in p.stdout, (p.stdout + p.stderr)[-3000:]
+        return
+    from p265_amd import _lib, digest
     params = R.make_params(pic_width=64, pic_height=64)
     distinct = [synth.make_picture(params, 970 + s, perf=bool(s % 2)) for s in range(4)]
     pd = R.params_dict(params)
     want = [digest.picture_digest(O.decode_picture(pd, p.as_oracle_dict())[1]) for p in distinct]
+    rounds = 4
     with recon_mod.ReconContext(params) as ctx:
-        n = int(ctx.describe()["num_cus"])
+        d = ctx.describe()
+        expect = os.environ.get("P265R_EXPECT_BUILD")
+        assert (d["phase_order"], d["early_residual"]) == {None: (0, 0), "phase_order": (1, 0),
+                                                           "early_residual": (0, 1)}[expect], d
+        n = int(d["num_cus"])
         big = [distinct[i % 4] for i in range(n)]
         small = [distinct[(i + 1) % 4] for i in range(4)]
         ctx.set_pipeline(3)
         bb, bs = ctx.upload(big), ctx.upload(small)
-        for _ in range(4):
+        assert 2 * rounds <= _lib.DIGEST_SLOTS
+        for r in range(rounds):
             ctx.run(bb)
-            ctx.run(bs)
-            ctx.run(bs)
-        ctx.sync()
-        for pics, b in ((big, bb), (small, bs)):
-            got = ctx.digest(b)
-            for i in range(len(pics)):
-                assert np.array_equal(got[i], want[distinct.index(pics[i])]), "picture %d of a %d-picture batch" % (i, len(pics))
+            ctx.digest_async(bb, r)
+            for k in range(2):
+                ctx.run(bs)
+                ctx.digest_async(bs, 2 * r + k)
+        for pics, b, slots in ((big, bb, rounds), (small, bs, 2 * rounds)):
+            got = ctx.digest_slots(b, slots)
+            for s_ in range(slots):
+                for i in range(len(pics)):
+                    assert np.array_equal(got[s_, i], want[distinct.index(pics[i])]), \
+                        "run %d, picture %d of a %d-picture batch" % (s_, i, len(pics))
             b.free()
 
 
