@@ -45,6 +45,11 @@ namespace p265r {
 #define P265R_HV_FAST 1
 #endif
 
+#ifdef P265R_ISA_MARK                    // tools/isa.sh: comment markers in the device assembly
+#define P265R_MARK(x) asm volatile("; MARK " x)
+#else
+#define P265R_MARK(x) do { } while (0)
+#endif
 #define P265R_GLOBAL __attribute__((address_space(1)))
 template <typename T>
 __device__ __forceinline__ const P265R_GLOBAL T* gptr(const T* p) { return (const P265R_GLOBAL T*)p; }
@@ -854,26 +859,31 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     // (pinned at the stage start: the read then shares the gather's LDS wait instead of adding one)
     auto ang = [&](uint32_t m) { uint32_t te = *lds32(tab + m * 64u + pos4); asm volatile("" : "+v"(te)); return te; };
     int rec = 0;
+    P265R_MARK("quad_stage0");
     {
         const uint32_t m = (w0 >> 17) & 63u;
         rec = quad_stage<0, CH>(rec, ext, lane, (int)m, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
                                 ang(m), r16, qid, xs, ys);
     }
+    P265R_MARK("quad_stage1");
     {
         const uint32_t m = (w0 >> 23) & 63u;
         rec = quad_stage<1, CH>(rec, ext, lane, (int)m, (w0 >> 30) & 1u, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
                                 ang(m), r16, qid, xs, ys);
     }
+    P265R_MARK("quad_stage2");
     {
         const uint32_t m = w1 & 63u;
         rec = quad_stage<2, CH>(rec, ext, lane, (int)m, (w1 >> 12) & 1u, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
                                 ang(m), r16, qid, xs, ys);
     }
+    P265R_MARK("quad_stage3");
     {
         const uint32_t m = (w1 >> 6) & 63u;
         rec = quad_stage<3, CH>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
                                 ang(m), r16, qid, xs, ys);
     }
+    P265R_MARK("quad_store");
     const uint32_t da = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
     *lds8(da) = (uint8_t)rec;
     if constexpr (CH) *lds8(da + 1024) = (uint8_t)(rec >> 16);
@@ -1293,6 +1303,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #pragma unroll P265R_JOB_UNROLL
 #endif
             for (int t = 0; t < nt; ++t) {
+                P265R_MARK("job_top");
                 if (t == t_trw) {                       // (a failed wait runs on; the loop exits after the job)
                     failed = !wait_up(need_tr);
                     if (XG) xg_copy(cts / 4 + 1, tr_k1);
@@ -1320,6 +1331,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #endif
                 }
                 const int sel = (int)((w0 >> 13) & 3u) | (((w0 >> 15) & 3u) ? 4 : 0);
+                P265R_MARK("job_dispatch");
 #ifdef P265R_PAD_SALU
                 {   // A/B probe: P265R_PAD_SALU dependent scalar adds per job (issue-bound test)
                     uint32_t z = w0;
@@ -1380,6 +1392,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                     default: recon_job<4, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
                   }
                 }
+                P265R_MARK("job_end");
 #ifdef P265R_JOB_STATS
                 {   // per job class: cycles (/16) and count, summed in LDS (RowCtrl::pad), P265R_DEBUG_SYNC prints
                     const int jc = (w5 & J5_QUAD) ? (((w0 >> 15) & 3u) ? 1 : 0)
