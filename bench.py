@@ -821,7 +821,10 @@ def main(argv=None):
     avg_launch_ms = acc["intra_ms"] / max(1, acc["intra_launches"])
     bytes_per_launch = intra_b / launches_per_step
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    traffic, prof_tag = measured_traffic(a.workload, "intra_rows_kernel", len(pics), avg_launch_ms)
+    if a.bit_depth == 8:
+        traffic, prof_tag = measured_traffic(a.workload, "intra_rows_kernel", len(pics), avg_launch_ms)
+    else:                                  # the 16-bit path's kernels have no committed PMC profile
+        traffic, prof_tag = None, "not profiled (Main 10 path)"
     cfg.update(batch_pipeline=a.pipeline, library=knobs)
     out = {
         "metric": METRIC,
@@ -837,11 +840,15 @@ def main(argv=None):
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
                                         % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_launch_ms, 4),
-                     "note": "achieved / avg_launch_ms: the batch alone, which runs the W = 12 build; the pipelined steps "
-                             "run W = 8 after their first (builds).  Bound by instruction issue (the CU's one scalar "
-                             "unit + each SIMD's VALU shared by 24 waves; waves park on s_waitcnt 42 % of their cycles "
-                             "while others issue), not by HBM (DESIGN.md §4); see issue_rates"},
-        "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms),
+                     "note": ("achieved / avg_launch_ms: the batch alone, which runs the W = 12 build; the pipelined steps "
+                              "run W = 8 after their first (builds: launches per build in the timed steps, and W = 8 "
+                              "alone).  Bound by instruction issue (the CU's one scalar unit + each SIMD's VALU shared "
+                              "by 24 waves; waves park on s_waitcnt 42 % of their cycles while others issue), not by "
+                              "HBM (DESIGN.md §4); see issue_rates" if a.bit_depth == 8 else
+                              "achieved / avg_launch_ms of one anti-diagonal launch (one workgroup per CTU of the "
+                              "diagonal, its TBs one after another): the Main 10 path, latency-bound, not the "
+                              "headline (DESIGN.md §4)")},
+        "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms) if a.bit_depth == 8 else None,
         "intra_jobs_per_launch": {"luma": jl, "chroma": jch},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
         "phase_gbs": {"residual": round(res_b / (acc["residual_ms"] / a.steps * 1e-3) / 1e9, 1),
@@ -854,7 +861,8 @@ def main(argv=None):
     if w8:
         builds["w8_alone"] = {"avg_launch_ms": round(w8, 4),
                               "frac": round(bytes_per_launch / (w8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    out["roofline"]["builds"] = builds
+    if a.bit_depth == 8:
+        out["roofline"]["builds"] = builds
     if a.workload == "c5":
         out["unit_latency_ms"] = c5_unit_latency(ctxs[0][0], cpu_sample, a.steps)
         if a.c5_world:
@@ -885,7 +893,7 @@ def main(argv=None):
         ceil = sc.get("copy_gbs") or sc["memcpy_d2d_gbs"]
         out["phase_gbs"]["vs_achievable_copy"] = {k: round(v / ceil, 3) for k, v in out["phase_gbs"].items()
                                                   if isinstance(v, float) and k != "whole_path_algorithmic"}
-        if a.workload == "c3" and launches_per_step == 1:
+        if a.workload == "c3" and launches_per_step == 1 and a.bit_depth == 8:
             out["roofline"]["issue"] = issue_ceiling(local, avg_launch_ms, jl + jch,
                                                      int(knobs.get("num_cus", 256)), out["issue_rates"])
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
