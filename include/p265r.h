@@ -130,7 +130,8 @@ typedef struct p265r_picture {
                                  1 = deblocking and SAO leave the block's samples untouched
                                  (pcm_loop_filter_disabled && pcm, or cu_transquant_bypass)   */
     void*            out[3];  /* decoded (post-deblocking, post-SAO) planes Y, Cb, Cr; stride =
-                                 plane width; uint8_t samples (8-bit).  NULL = do not download */
+                                 plane width in samples; uint8_t samples at BitDepth 8, uint16_t
+                                 at 9..10.  NULL = do not download                              */
     void*            recon[3];/* optional in-loop-filter input (reconstruction before deblocking
                                  and SAO), same layout; NULL = skip.  Written by download, or
                                  read by upload with P265R_PIC_RECON_INPUT                     */
