@@ -32,16 +32,24 @@ struct Nal {
 };
 
 // Split an Annex-B byte stream at start codes (0x000001 / 0x00000001), dropping
-// trailing_zero_8bits, and convert each NAL unit payload to RBSP (7.3.1.1, 7.4.2).
+// trailing_zero_8bits, and convert each NAL unit payload to RBSP (7.3.1.1, 7.4.2).  Zero bytes are
+// found with memchr and the bytes between emulation_prevention_three_bytes are block-copied (the
+// split runs on one thread ahead of the parallel slice-data parse).
 inline std::vector<Nal> split_nals(const uint8_t* d, size_t n) {
     std::vector<Nal> out;
-    size_t i = 0;
+    // first k >= from with d[k..k+2] == 00 00 01 (n if none)
     auto find_sc = [&](size_t from) -> size_t {
-        for (size_t k = from; k + 2 < n; ++k)
-            if (d[k] == 0 && d[k + 1] == 0 && d[k + 2] == 1) return k;
+        size_t k = from;
+        while (k + 2 < n) {
+            const void* z = std::memchr(d + k, 0, n - 2 - k);
+            if (!z) return n;
+            k = (size_t)(static_cast<const uint8_t*>(z) - d);
+            if (d[k + 1] == 0 && d[k + 2] == 1) return k;
+            ++k;
+        }
         return n;
     };
-    i = find_sc(0);
+    size_t i = find_sc(0);
     while (i < n) {
         size_t start = i + 3;
         size_t next = find_sc(start);
@@ -55,14 +63,25 @@ inline std::vector<Nal> split_nals(const uint8_t* d, size_t n) {
             nal.layer_id = (h >> 3) & 63;
             nal.temporal_id = (int)(h & 7) - 1;
             if (nal.temporal_id < 0) bs_fail("nuh_temporal_id_plus1 == 0");
-            nal.rbsp.reserve(end - start);
-            int zeros = 0;
-            for (size_t k = start + 2; k < end; ++k) {
-                uint8_t b = d[k];
-                if (zeros >= 2 && b == 3) { zeros = 0; continue; }  // emulation_prevention_three_byte
-                zeros = (b == 0) ? zeros + 1 : 0;
-                nal.rbsp.push_back(b);
+            nal.rbsp.resize(end - start - 2);
+            uint8_t* o = nal.rbsp.data();
+            size_t k = start + 2;
+            while (k < end) {
+                // next 00 00 03 at p >= k (a removed 03 resets the zero count: the search restarts after it)
+                size_t p = k;
+                size_t cut = end;
+                while (p + 2 < end) {
+                    const void* z = std::memchr(d + p, 0, end - 2 - p);
+                    if (!z) break;
+                    p = (size_t)(static_cast<const uint8_t*>(z) - d);
+                    if (d[p + 1] == 0 && d[p + 2] == 3) { cut = p + 2; break; }
+                    ++p;
+                }
+                std::memcpy(o, d + k, cut - k);                   // up to (not including) the 03
+                o += cut - k;
+                k = cut < end ? cut + 1 : end;
             }
+            nal.rbsp.resize((size_t)(o - nal.rbsp.data()));
             out.push_back(std::move(nal));
         }
         i = next;

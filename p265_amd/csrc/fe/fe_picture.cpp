@@ -193,10 +193,12 @@ public:
         ct_depth_.assign((size_t)min_cb_w_ * min_cb_h_, 0);
         qp_map_.assign((size_t)min_cb_w_ * min_cb_h_, 0);
         ipm_.assign((size_t)w4_ * h4_, 1);
-        ctu_tbs_.assign(a.size_ctb, {});
         // every sample is covered by at most one coded TB (or PCM block) per component: the dense
-        // blocks are carved from one arena sized once (uninitialised; trimmed in finish())
+        // blocks are carved from one arena sized once (uninitialised; trimmed in finish()); the TB
+        // array is reserved for its bound (one luma TB per 4 x 4 and a chroma pair per 8 x 8) and
+        // filled in decode order, each CTU's TBs contiguous
         out_.coef.resize((size_t)sps_.width * sps_.height * 3 / 2 + 1024);
+        out_.tbs.reserve((size_t)w4_ * h4_ * 3 / 2 + 64);
         coef_used_ = 0;
         out_.ctus.assign(a.size_ctb, p265r_ctu{});
         for (auto& c : out_.ctus) c.flags = P265R_CTU_LF_ACROSS_SLICES;
@@ -289,16 +291,23 @@ public:
         out_.coef.resize(coef_used_);
         for (int rs = 0; rs < a_.size_ctb; ++rs)
             if (ctb_slice_[rs] < 0) bs_fail("picture incomplete: CTB not covered by any slice segment");
-        size_t total = 0;
-        for (auto& v : ctu_tbs_) total += v.size();
-        out_.tbs.clear();
-        out_.tbs.reserve(total);
-        for (int rs = 0; rs < a_.size_ctb; ++rs) {
-            auto& v = ctu_tbs_[rs];
-            if (v.size() > 0xFFFF) bs_fail("too many TBs in a CTU");
-            out_.ctus[rs].tb_begin = (uint32_t)out_.tbs.size();
-            out_.ctus[rs].tb_count = (uint16_t)v.size();
-            out_.tbs.insert(out_.tbs.end(), v.begin(), v.end());
+        // TBs were emitted in decode (tile-scan) order; the records list them by raster CTU
+        bool raster = true;
+        size_t next = 0;
+        for (int rs = 0; rs < a_.size_ctb && raster; ++rs) {
+            raster = out_.ctus[rs].tb_begin == next;
+            next += out_.ctus[rs].tb_count;
+        }
+        if (!raster) {
+            std::vector<p265r_tb, PoolAlloc<p265r_tb>> v;
+            v.reserve(out_.tbs.size());
+            for (int rs = 0; rs < a_.size_ctb; ++rs) {
+                p265r_ctu& c = out_.ctus[rs];
+                const size_t b = c.tb_begin;
+                c.tb_begin = (uint32_t)v.size();
+                v.insert(v.end(), out_.tbs.begin() + b, out_.tbs.begin() + b + c.tb_count);
+            }
+            out_.tbs.swap(v);
         }
     }
 
@@ -337,7 +346,12 @@ private:
         cur_ctu_ = rs;
         int cx = rs % W_, cy = rs / W_;
         if (h.sao_luma || h.sao_chroma) parse_sao(rs, ts, cx, cy, c);
+        const size_t tb0 = out_.tbs.size();
         coding_quadtree(cx << log2ctb_, cy << log2ctb_, log2ctb_, 0);
+        const size_t ntb = out_.tbs.size() - tb0;
+        if (ntb > 0xFFFF) bs_fail("too many TBs in a CTU");
+        c.tb_begin = (uint32_t)tb0;
+        c.tb_count = (uint16_t)ntb;
     }
 
     // sao(rx, ry) (7.3.8.3; sao.py:15-136), SaoOffsetVal with EO signs inferred (7.4.9.3.2)
@@ -567,10 +581,9 @@ private:
         int qcb = qpc_from_qpi(clip3(-qp_bd_c_, 57, qpy + pps_.cb_qp_offset + hdr_->cb_qp_offset)) + qp_bd_c_;
         int qcr = qpc_from_qpi(clip3(-qp_bd_c_, 57, qpy + pps_.cr_qp_offset + hdr_->cr_qp_offset)) + qp_bd_c_;
         uint8_t qps[3] = {(uint8_t)(qpy + qp_bd_y_), (uint8_t)qcb, (uint8_t)qcr};
-        auto& dst = ctu_tbs_[cur_ctu_];
         for (auto& t : cu_tbs_) {
             t.qp = qps[t.c_idx];
-            dst.push_back(t);
+            out_.tbs.push_back(t);
         }
         if (cu_bypass_ || (pcm && sps_.pcm_loop_filter_disabled)) mark_nofilter(x0, y0, log2);
     }
@@ -749,15 +762,18 @@ private:
                 if (xs + 1 < sbw) prev |= csbf[xs + 1][ys];
                 if (ys + 1 < sbw) prev |= csbf[xs][ys + 1] << 1;
                 const uint8_t* sctx = kSigCtx.t[cc][log2 - 2][scan][prev][(xs | ys) == 0 ? 1 : 0];
-                for (int nn = start; nn >= 0; --nn) {
-                    if (nn > 0 || !infer_dc) {
-                        if (e.decision(cx[sctx[nn]])) {
-                            sig_pos[nsig++] = nn;
-                            infer_dc = 0;
-                        }
-                    } else {
-                        sig_pos[nsig++] = 0;   // DC of a coded sub-block with no other significant coefficient
-                    }
+                // branch-free on the decoded bins (an LPS-rate branch mispredicts on every few bins)
+                for (int nn = start; nn > 0; --nn) {
+                    const int b = e.decision(cx[sctx[nn]]);
+                    sig_pos[nsig] = nn;
+                    nsig += b;
+                    infer_dc &= b ^ 1;
+                }
+                if (start >= 0) {
+                    // DC: decoded, or inferred significant when no other coefficient of the coded sub-block is
+                    const int b = infer_dc ? 1 : e.decision(cx[sctx[0]]);
+                    sig_pos[nsig] = 0;
+                    nsig += b;
                 }
             }
             if (nsig == 0) continue;
@@ -771,13 +787,12 @@ private:
             int ng1 = std::min(nsig, 8);
             const int g1_base = C_GT1 + ctx_set * 4 + (c ? 16 : 0);
             for (int k = 0; k < ng1; ++k) {
-                g1[k] = e.decision(cx[g1_base + greater1_state]);
-                if (g1[k]) {
-                    greater1_state = 0;
-                    if (first_g1_idx < 0) first_g1_idx = k;
-                } else if (greater1_state > 0 && greater1_state < 3) {
-                    ++greater1_state;
-                }
+                const int b = e.decision(cx[g1_base + greater1_state]);
+                g1[k] = b;
+                // (9.3.4.2.6) greater1Ctx: 0 after a 1, else 1 -> 2 -> 3 (saturating); branch-free
+                const int inc = (greater1_state > 0) & (greater1_state < 3);
+                greater1_state = b ? 0 : greater1_state + inc;
+                first_g1_idx = (first_g1_idx < 0 && b) ? k : first_g1_idx;
             }
             if (first_g1_idx >= 0) g2[first_g1_idx] = e.decision(cx[C_GT2 + ctx_set + (c ? 4 : 0)]);
             bool hidden = sdh && (sig_pos[0] - sig_pos[nsig - 1] > 3);
@@ -832,7 +847,6 @@ private:
     std::vector<uint8_t> ct_depth_;
     std::vector<int8_t> qp_map_;
     std::vector<uint8_t> ipm_;
-    std::vector<std::vector<p265r_tb>> ctu_tbs_;
     std::vector<p265r_tb> cu_tbs_;
     size_t coef_used_ = 0;
     const SliceHeader* hdr_ = nullptr;
