@@ -100,6 +100,26 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ lds_u8* lds8(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
 __device__ __forceinline__ lds_u32* lds32(uint32_t a) { return (lds_u32*)(uintptr_t)a; }
+// sample T (uint8_t, or uint16_t for BitDepth 9..10) at SAMPLE address s (byte address s * sizeof(T)): the
+// job functions compute their LDS addresses in sample units, so one formula serves both sample sizes
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T* ldsT(uint32_t s) {
+    return (__attribute__((address_space(3))) T*)(uintptr_t)(s * (uint32_t)sizeof(T));
+}
+
+// Packed Cb | Cr << 16 arithmetic of the chroma jobs: w x both halves.  8-bit samples packed at 16-bit
+// spacing stay below 2^24, so one v_mul_u32_u24 weighs both; 10-bit ones do not, and take the packed
+// 16-bit multiply (every weighted sum of the chroma predictors stays below 2^16 per half at 10 bits too)
+template <typename T>
+__device__ __forceinline__ uint32_t pmul(uint32_t w, uint32_t packed) {
+    if constexpr (sizeof(T) == 1) {
+        return __umul24(w, packed);
+    } else {
+        uint32_t r;
+        asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(w * 0x00010001u), "v"(packed));
+        return r;
+    }
+}
 
 // Signed 24-bit product (both |operands| < 2^23): the projected-reference index r * invAngle
 // (8.4.4.2.6), which LLVM otherwise widens to a quarter-rate v_mul_lo_u32 once it knows both
@@ -160,21 +180,24 @@ __device__ __forceinline__ uint32_t angtab_entry(int m, int p) {
     return a | b << 8 | (uint32_t)fact << 16 | (uint32_t)(32 - fact) << 24;
 }
 
-struct WaveLds {                 // one wave's private CTU state (4564 B): a wave holds one row
-    uint8_t  ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
-    union {                      // ref: raw / final linear reference arrays (8-bit samples)
+template <typename T>            // sample type: uint8_t (BitDepth 8), uint16_t (9..10)
+struct WaveLdsT {                // one wave's private CTU state (4564 B at 8 bits): a wave holds one row
+    T        ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
+    union {                      // ref: raw / final linear reference arrays
         struct {
-            uint8_t y[64 * 64];          // interior luma, stride 64
-            uint8_t yleft[64];           // right column of the previous CTU of this row
-            uint8_t ytop[132];           // XG: the row above, [4 + x] for x = -4 .. 2 CTB - 1
+            T y[64 * 64];                // interior luma, stride 64
+            T yleft[64];                 // right column of the previous CTU of this row
+            T ytop[sizeof(T) == 1 ? 132 : 136];   // XG: the row above, [4 + x] for x = -4 .. 2 CTB - 1
+                                                  // (16-bit: padded so consecutive waves stay 16-B aligned)
         };
         struct {
-            uint8_t c[2][32 * 32];       // interior chroma, stride 32
-            uint8_t cleft[2][32];
-            uint8_t ctop[2][68];         // XG: per plane as ytop
+            T c[2][32 * 32];             // interior chroma, stride 32
+            T cleft[2][32];
+            T ctop[2][68];               // XG: per plane as ytop
         };
     };
 };
+using WaveLds = WaveLdsT<uint8_t>;
 // timing experiment (wrong output): every residual load of the row kernel inside one 8-KB window
 #ifdef P265R_RES_FAKE
 #define P265R_RI(x) ((x) & 4095)
@@ -197,9 +220,14 @@ struct WaveLds {                 // one wave's private CTU state (4564 B): a wav
 #define P265R_TR_DEFER 1                 // 0: wait for the top-right CTU before the CTU starts (A/B knob)
 #endif
 // job word w0 addresses a TB origin as yr * 64 + xr (luma) or 4096 + yr * 32 + xr (chroma,
-// intra_prep.h); WaveLds byte of that origin = w0 offset + kOrg[chroma]
-constexpr uint32_t kOrgL = offsetof(WaveLds, y);
-constexpr uint32_t kOrgC = (uint32_t)offsetof(WaveLds, c) - 4096u;
+// intra_prep.h); WaveLds sample of that origin = w0 offset + kOrg[chroma] (sample units: bytes at 8 bits)
+template <typename T> constexpr uint32_t kOrgLT = (uint32_t)(offsetof(WaveLdsT<T>, y) / sizeof(T));
+template <typename T> constexpr uint32_t kOrgCT = (uint32_t)(offsetof(WaveLdsT<T>, c) / sizeof(T)) - 4096u;
+template <typename T> constexpr uint32_t kRefT = (uint32_t)(offsetof(WaveLdsT<T>, ref) / sizeof(T));
+template <typename T> constexpr uint32_t kYLeftT = (uint32_t)(offsetof(WaveLdsT<T>, yleft) / sizeof(T));
+template <typename T> constexpr uint32_t kCLeftT = (uint32_t)(offsetof(WaveLdsT<T>, cleft) / sizeof(T));
+constexpr uint32_t kOrgL = kOrgLT<uint8_t>;
+constexpr uint32_t kOrgC = kOrgCT<uint8_t>;
 
 struct RowCtrl {                 // 256 B at the start of dynamic LDS
     int next_row;
@@ -265,9 +293,9 @@ __device__ __forceinline__ int wave_sum(int v, int half) {
 // neighbourhood (CTU interior, left column, line buffer), every lane reading the sample
 // that substitutes its entry (availability comes precomputed per 4-luma-sample unit),
 // so substitution costs no extra round trip; luma filtering (8.4.4.2.3) adds one.
-template <int LOG2, bool PAIR>
-__device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, uint32_t w0, uint32_t w1,
-                                          uint32_t w2, uint4 ra, uint4 rb, int lane) {
+template <int LOG2, bool PAIR, typename T = uint8_t>
+__device__ __forceinline__ void recon_job(WaveLdsT<T>& L, const T* line_top, uint32_t w0, uint32_t w1,
+                                          uint32_t w2, uint4 ra, uint4 rb, int lane, int maxv = 255) {
     constexpr int n = 1 << LOG2;
     constexpr int nn = n * n;
     constexpr int LANES = PAIR ? 32 : 64;
@@ -276,15 +304,16 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
     constexpr int NCH = (nref + LANES - 1) / LANES;
     constexpr int US = PAIR ? 1 : 2;                      // log2 availability unit (samples)
     constexpr int NU = (2 * n) >> US;                     // units per side
-    constexpr int maxv = 255;                             // 8-bit samples (P265R_EUNSUPPORTED otherwise)
+    constexpr int SPW = 4 / (int)sizeof(T);               // samples per 32-bit word
+    const int half_v = (maxv + 1) >> 1;                   // 1 << (BitDepth - 1): no reference available
     const int hl = PAIR ? (lane & 31) : lane;
     const int half = PAIR ? (lane >> 5) : 0;
     const int ofs = (int)(w0 & 0x1fffu);
     const int xr = PAIR ? ((ofs - 4096) & 31) : (ofs & 63);
     const int yr = PAIR ? ((ofs - 4096) >> 5) : (ofs >> 6);
     constexpr int ist = PAIR ? 32 : 64;
-    uint8_t* const org = reinterpret_cast<uint8_t*>(&L) + (PAIR ? kOrgC : kOrgL) + ofs + half * 1024;   // TB origin
-    const uint8_t* const lcol = (PAIR ? L.cleft[half] : L.yleft) + yr;
+    T* const org = reinterpret_cast<T*>(&L) + (PAIR ? kOrgCT<T> : kOrgLT<T>) + ofs + half * 1024;   // TB origin
+    const T* const lcol = (PAIR ? L.cleft[half] : L.yleft) + yr;
     const int mode = (int)((w0 >> 17) & 63u);
     const bool own = hl * S < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
     const int sidx = hl * S < nn ? hl * S : 0;
@@ -304,10 +333,12 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
         rw[0] = (e & 1) ? (wd >> 16) : (wd & 0xffffu);
     }
     auto resv = [&](int i) { return (int)(int16_t)(rw[i >> 1] >> ((i & 1) * 16)); };
-    uint32_t outw[(S + 3) / 4];
+    uint32_t outw[(S + SPW - 1) / SPW];
 #pragma unroll
-    for (int q = 0; q < (S + 3) / 4; ++q) outw[q] = 0;
-    auto put = [&](int i, int v) { outw[i >> 2] |= (uint32_t)clip_pel(v + resv(i), maxv) << (8 * (i & 3)); };
+    for (int q = 0; q < (S + SPW - 1) / SPW; ++q) outw[q] = 0;
+    auto put = [&](int i, int v) {
+        outw[i / SPW] |= (uint32_t)clip_pel(v + resv(i), maxv) << (8 * (int)sizeof(T) * (i % SPW));
+    };
 
     if (w0 & J_PCM) {
 #pragma unroll
@@ -315,13 +346,13 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
     } else {
         // ---- gather (+ substitution) --------------------------------------------------
         const int filt = PAIR ? 0 : (int)((w0 >> 24) & 3u);
-        uint8_t* const R0 = PAIR ? L.ref[half] : L.ref[0];
-        uint8_t* const RF = (PAIR || !filt) ? R0 : L.ref[1];
+        T* const R0 = PAIR ? L.ref[half] : L.ref[0];
+        T* const RF = (PAIR || !filt) ? R0 : L.ref[1];
         // sources: left column (entries 0..2n-1), corner (2n), top row (2n+1..4n)
-        const uint8_t* const lbase = xr == 0 ? lcol : org - 1;
+        const T* const lbase = xr == 0 ? lcol : org - 1;
         const int lstep = xr == 0 ? 1 : ist;
-        const uint8_t* const tbase = yr == 0 ? line_top + xr : org - ist;
-        const uint8_t* const cptr = yr == 0 ? line_top + xr - 1 : (xr == 0 ? lcol - 1 : org - ist - 1);
+        const T* const tbase = yr == 0 ? line_top + xr : org - ist;
+        const T* const cptr = yr == 0 ? line_top + xr - 1 : (xr == 0 ? lcol - 1 : org - ist - 1);
         const unsigned long long m = (unsigned long long)w2 | ((unsigned long long)((w1 >> 21) & 1u) << 32);
         const bool all = w0 & J_ALL, none = w0 & J_NONE;
         int dcs = 0;
@@ -340,9 +371,9 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                     const int sf = uf < NU ? (uf << US) : (uf == NU ? 2 * n : 2 * n + 1 + ((uf - NU - 1) << US));
                     s = ((m >> u) & 1ull) ? k : (below ? sb : sf);
                 }
-                const uint8_t* src = s < 2 * n ? lbase + (2 * n - 1 - s) * lstep : (s == 2 * n ? cptr : tbase + (s - 2 * n - 1));
-                const int v = none ? 128 : (int)*src;
-                R0[k] = (uint8_t)v;
+                const T* src = s < 2 * n ? lbase + (2 * n - 1 - s) * lstep : (s == 2 * n ? cptr : tbase + (s - 2 * n - 1));
+                const int v = none ? half_v : (int)*src;
+                R0[k] = (T)v;
                 if ((k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n)) dcs += v;
             }
         }
@@ -353,7 +384,8 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
             int corner = 0, bl = 0, tr = 0;
             if (n == 32 && filt == 2) {
                 corner = R0[2 * n]; bl = R0[0]; tr = R0[4 * n];
-                strong = abs(corner + tr - 2 * (int)R0[3 * n]) < 8 && abs(corner + bl - 2 * (int)R0[n]) < 8;
+                const int thr = (maxv + 1) >> 5;                  // 1 << (BitDepth - 5)
+                strong = abs(corner + tr - 2 * (int)R0[3 * n]) < thr && abs(corner + bl - 2 * (int)R0[n]) < thr;
             }
 #pragma unroll
             for (int jj = 0; jj < NCH; ++jj) {
@@ -370,12 +402,12 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
                             f = ((int)R0[k - 1] + 2 * f + (int)R0[k + 1] + 2) >> 2;
                         }
                     }
-                    RF[k] = (uint8_t)f;
+                    RF[k] = (T)f;
                 }
             }
             wave_sync();
         }
-        const uint8_t* const R = RF;
+        const T* const R = RF;
         // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------
         if (mode == 0) {
             const int trs = R[3 * n + 1], bls = R[n - 1];
@@ -435,12 +467,17 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
         }
     }
     if (own) {
-        uint8_t* dst = org + sy * ist + sx;
-        if constexpr (S == 16) *reinterpret_cast<uint4*>(dst) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
-        else if constexpr (S == 8) *reinterpret_cast<uint2*>(dst) = make_uint2(outw[0], outw[1]);
-        else if constexpr (S == 4) *reinterpret_cast<uint32_t*>(dst) = outw[0];
-        else if constexpr (S == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)outw[0];
-        else dst[0] = (uint8_t)outw[0];
+        T* dst = org + sy * ist + sx;
+        constexpr int NB = S * (int)sizeof(T);                 // bytes per lane, naturally aligned
+        if constexpr (NB == 32) {
+            reinterpret_cast<uint4*>(dst)[0] = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+            reinterpret_cast<uint4*>(dst)[1] = make_uint4(outw[4], outw[5], outw[6], outw[7]);
+        }
+        else if constexpr (NB == 16) *reinterpret_cast<uint4*>(dst) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+        else if constexpr (NB == 8) *reinterpret_cast<uint2*>(dst) = make_uint2(outw[0], outw[1]);
+        else if constexpr (NB == 4) *reinterpret_cast<uint32_t*>(dst) = outw[0];
+        else if constexpr (NB == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)outw[0];
+        else dst[0] = (T)outw[0];
     }
     wave_sync();
 }
@@ -451,9 +488,9 @@ __device__ __forceinline__ void recon_job(WaveLds& L, const uint8_t* line_top, u
 // TAB: angw is instead this lane's entry of the workgroup's 4x4 angular table (AngTab4: both
 // reference indices and the weights, no projection arithmetic); modes 10 / 26 are told by number.
 template <int LOG2, bool PAIR, bool TAB = false>
-__device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, int y, int k, int hl, int half) {
+__device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, int y, int k, int hl, int half,
+                                         int maxv = 255) {
     constexpr int n = 1 << LOG2;
-    constexpr int maxv = 255;
     const int base = half * 32;                                  // first reference lane of this half
     auto ref = [&](int i) { return __builtin_amdgcn_ds_bpermute((base + i) << 2, v); };
     auto uref = [&](int i) {                                     // reference i of this lane's half, uniform per half
@@ -527,12 +564,13 @@ __device__ __forceinline__ int fast_pred(int mode, uint32_t angw, int v, int x, 
 // needs one LDS read, one bpermute round trip (two with the 8x8 [1 2 1] filter) and one
 // LDS write - no reference array in LDS and no divergent control flow.  r16 = this
 // lane's residual sample as loaded (ignored when the TB has none).
-template <int LOG2, bool PAIR>
+template <int LOG2, bool PAIR, typename T = uint8_t>
 __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1,
-                                           uint32_t w5, int r16, int lane, uint32_t tab) {
+                                           uint32_t w5, int r16, int lane, uint32_t tab, int maxv = 255) {
     constexpr int n = 1 << LOG2;
     constexpr int nn = n * n;
-    constexpr int maxv = 255;
+    constexpr uint32_t PB = sizeof(T);
+    lbase /= PB; line_top /= PB;                            // byte -> sample addresses
     const int hl = PAIR ? (lane & 31) : lane;
     const int half = PAIR ? (lane >> 5) : 0;
     const int ofs = (int)(w0 & 0x1fffu);
@@ -545,8 +583,8 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     const int k = min(hl, 4 * n);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
     const int sref = min(max(k, fa), la);
-    const uint32_t orgA = lbase + (PAIR ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)half * 1024u;   // TB origin
-    const uint32_t lcolA = lbase + (uint32_t)(PAIR ? offsetof(WaveLds, cleft) + half * 32 : offsetof(WaveLds, yleft)) + (uint32_t)yr;
+    const uint32_t orgA = lbase + (PAIR ? kOrgCT<T> : kOrgLT<T>) + (uint32_t)ofs + (uint32_t)half * 1024u;   // TB origin
+    const uint32_t lcolA = lbase + (PAIR ? kCLeftT<T> + (uint32_t)half * 32u : kYLeftT<T>) + (uint32_t)yr;
     const uint32_t ltA = line_top + (uint32_t)xr;
     // left refs k < 2n at lb - k * ls, top refs k > 2n at tb + k; the corner k = 2n follows the
     // left formula inside the CTU / left column and the top formula in the line buffer (yr = 0)
@@ -555,7 +593,7 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     const uint32_t tb = (yr == 0 ? ltA : orgA - ist) - 2 * n - 1;
     const int th = 2 * n + (yr > 0 ? 1 : 0);
     const uint32_t sa = tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
-    const int raw = (int)*lds8(sa);
+    const int raw = (int)*ldsT<T>(sa);
     // luma: this sample's angular table entry (AngTab4 / AngTab8), read together with the gather
     constexpr bool TAB = !PAIR && (LOG2 == 2 || (LOG2 == 3 && P265R_ANGTAB8));
     uint32_t te = w1;
@@ -564,7 +602,7 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
         te = *lds32(t0 + (uint32_t)mode * (uint32_t)(nn * 4) + (uint32_t)((hl & (nn - 1)) * 4));
         asm volatile("" : "+v"(te));
     }
-    int v = (w0 & J_NONE) ? 128 : raw;
+    int v = (w0 & J_NONE) ? (maxv + 1) >> 1 : raw;
     if (!PAIR && LOG2 == 3 && ((w0 >> 24) & 3u)) {           // [1 2 1] (8.4.4.2.3), 8x8: never strong
         // neighbours k -/+ 1 by DPP wave shifts (lane k holds sample k for k <= 4n; no LDS round trip)
         const int vl = wave_from_prev(v), vr = wave_from_next(v);
@@ -574,28 +612,31 @@ __device__ __forceinline__ void recon_fast(uint32_t lbase, uint32_t line_top, ui
     // ---- prediction (8.4.4.2.4-6) fused with reconstruction (8.6.7) ---------------------------
     const int sidx = hl < nn ? hl : 0;
     const int x = sidx & (n - 1), y = sidx >> LOG2;
-    const int pred = fast_pred<LOG2, PAIR, TAB>(mode, te, v, x, y, k, hl, half);
+    const int pred = fast_pred<LOG2, PAIR, TAB>(mode, te, v, x, y, k, hl, half, maxv);
     // every lane stores (no exec-mask juggling): lanes without a sample of this job write a
-    // private byte of the (here unused) reference scratch area
+    // private sample of the (here unused) reference scratch area
     const bool own = hl < nn && (!PAIR || ((w0 >> (15 + half)) & 1u));
-    const uint32_t da = own ? orgA + y * ist + x : lbase + (uint32_t)offsetof(WaveLds, ref) + lane;
+    const uint32_t da = own ? orgA + y * ist + x : lbase + kRefT<T> + lane;
     // r16: the loaded sample (an uncoded half reads the zero block, intra_prep.h w3/w4)
-    *lds8(da) = (uint8_t)clip_pel(pred + r16, maxv);
+    *ldsT<T>(da) = (T)clip_pel(pred + r16, maxv);
     wave_sync();
 }
 
 // Fast 16x16 luma job (J5_FAST): as recon_fast, 65 reference samples (lane k holds
 // sample k, sample 64 is wave-uniform), 4 predicted samples per lane (a row quarter),
 // residual (4 samples) in rw.x / rw.y, one 4-byte LDS store per lane.
+template <typename T = uint8_t>
 __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, uint32_t w0, uint32_t w1,
-                                             uint32_t w5, uint4 rw, int lane) {
-    constexpr int n = 16, LOG2 = 4, ist = 64, maxv = 255;
+                                             uint32_t w5, uint4 rw, int lane, int maxv = 255) {
+    constexpr int n = 16, LOG2 = 4, ist = 64;
+    constexpr uint32_t PB = sizeof(T);
+    lbase /= PB; line_top /= PB;                            // byte -> sample addresses
     const int ofs = (int)(w0 & 0x1fffu);
     const int xr = ofs & 63, yr = ofs >> 6;
     const int mode = (int)((w0 >> 17) & 63u);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
-    const uint32_t orgA = lbase + kOrgL + (uint32_t)ofs;
-    const uint32_t lcolA = lbase + (uint32_t)offsetof(WaveLds, yleft) + (uint32_t)yr;
+    const uint32_t orgA = lbase + kOrgLT<T> + (uint32_t)ofs;
+    const uint32_t lcolA = lbase + kYLeftT<T> + (uint32_t)yr;
     const uint32_t ltA = line_top + (uint32_t)xr;
     const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
     const int ls = xr == 0 ? 1 : ist;
@@ -603,11 +644,12 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
     const int th = 2 * n + (yr > 0 ? 1 : 0);
     auto addr = [&](int sref) { return tb + sref + (sref < th ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u); };
     const bool none = (w0 & J_NONE) != 0;
+    const int half_v = (maxv + 1) >> 1;
     const int k = lane;
-    const int raw = (int)*lds8(addr(min(max(k, fa), la)));
-    const int raw64 = (int)*lds8(addr(min(max(4 * n, fa), la)));
-    int v = none ? 128 : raw;
-    const int r64 = none ? 128 : __builtin_amdgcn_readfirstlane(raw64);     // reference sample 64 (end, unfiltered)
+    const int raw = (int)*ldsT<T>(addr(min(max(k, fa), la)));
+    const int raw64 = (int)*ldsT<T>(addr(min(max(4 * n, fa), la)));
+    int v = none ? half_v : raw;
+    const int r64 = none ? half_v : __builtin_amdgcn_readfirstlane(raw64);     // reference sample 64 (end, unfiltered)
     if ((w0 >> 24) & 3u) {                                    // [1 2 1] (8.4.4.2.3)
         const int vl = wave_from_prev(v), vr0 = wave_from_next(v);   // DPP wave shifts
         const int vr = k == 63 ? r64 : vr0;
@@ -686,14 +728,16 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
             }
         }
     }
-    uint32_t out = 0;                                         // (an uncoded TB's residual is the zero block)
+    uint32_t out[2] = {0u, 0u};                               // (an uncoded TB's residual is the zero block)
+    constexpr int SPW = 4 / (int)PB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t wd = i < 2 ? rw.x : rw.y;
         const int res = (int)(int16_t)(wd >> (16 * (i & 1)));
-        out |= (uint32_t)clip_pel(pred[i] + res, maxv) << (8 * i);
+        out[i / SPW] |= (uint32_t)clip_pel(pred[i] + res, maxv) << (8 * (int)PB * (i % SPW));
     }
-    *lds32(orgA + y * ist + x0) = out;
+    if constexpr (PB == 1) *lds32(orgA + y * ist + x0) = out[0];
+    else *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(ldsT<T>(orgA + y * ist + x0)) = u32x2_t{out[0], out[1]};
     wave_sync();
 }
 
@@ -703,7 +747,7 @@ __device__ __forceinline__ void recon_fast16(uint32_t lbase, uint32_t line_top, 
 // below 2^16 per half (planar / DC 2n x 255 + n, angular 32 x 255 + 16), so the halves never
 // carry into each other and one shift + mask divides both.  Lane k of v holds reference k of
 // 8.4.4.2.2's linear order.  Chroma (4:2:0) has no DC / horizontal / vertical boundary smoothing.
-template <int LOG2, bool TAB = false>
+template <int LOG2, bool TAB = false, typename T = uint8_t>
 __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, int x, int y, int k) {
     constexpr int n = 1 << LOG2;
     constexpr uint32_t rnd = (uint32_t)n * 0x00010001u;
@@ -714,7 +758,7 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
         if (TAB) {                                             // AngTab4 entry (modes 10 / 26 included: fact 0)
             const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), (int)v);
             const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), (int)v);
-            return ((__umul24(angw >> 24, a) + __umul24((angw >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+            return ((pmul<T>(angw >> 24, a) + pmul<T>((angw >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
         }
         if (P265R_HV_FAST && (angw & 0xffu) == 0u)              // modes 10 / 26: a copy (no chroma smoothing)
             return ref(mode >= 18 ? 2 * n + 1 + x : 2 * n - 1 - y);
@@ -727,12 +771,12 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
         const int idx = pa >> 5, fact = pa & 31;
         const int nr0 = -1 - across - idx;
         const uint32_t a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(ang_ref<2 * n>(nr0 - 1, ia, ns));
-        return ((__umul24(32 - fact, a) + __umul24(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+        return ((pmul<T>(32 - fact, a) + pmul<T>(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
     }
     if (mode == 0) {
         const uint32_t lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);
-        const uint32_t s = __umul24(n - 1 - x, lft) + __umul24(x + 1, uref(3 * n + 1)) + __umul24(n - 1 - y, top) +
-                           __umul24(y + 1, uref(n - 1)) + rnd;
+        const uint32_t s = pmul<T>(n - 1 - x, lft) + pmul<T>(x + 1, uref(3 * n + 1)) + pmul<T>(n - 1 - y, top) +
+                           pmul<T>(y + 1, uref(n - 1)) + rnd;
         return (s >> (LOG2 + 1)) & msk;
     }
     const bool in = (k >= n && k < 2 * n) || (k > 2 * n && k <= 3 * n);
@@ -740,10 +784,10 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
     return (s >> (LOG2 + 1)) & msk;
 }
 
-// Clip1(pred + res) of both halves: pred packed (0..255 per half), res two int16 residuals
-__device__ __forceinline__ uint32_t cquad_recon(uint32_t pred, uint32_t res) {
-    const int cb = clip_pel((int)(pred & 0xffffu) + (int)(int16_t)(res & 0xffffu), 255);
-    const int cr = clip_pel((int)(pred >> 16) + ((int)res >> 16), 255);
+// Clip1(pred + res) of both halves: pred packed (0..maxv per half), res two int16 residuals
+__device__ __forceinline__ uint32_t cquad_recon(uint32_t pred, uint32_t res, int maxv = 255) {
+    const int cb = clip_pel((int)(pred & 0xffffu) + (int)(int16_t)(res & 0xffffu), maxv);
+    const int cr = clip_pel((int)(pred >> 16) + ((int)res >> 16), maxv);
     return (uint32_t)cb | (uint32_t)cr << 16;
 }
 
@@ -753,17 +797,20 @@ __device__ __forceinline__ uint32_t cquad_recon(uint32_t pred, uint32_t res) {
 // interior, 32 B in the left column, cw B in the line buffer); lane l predicts sample
 // (l & 7, l >> 3) of both.  r32 = this lane's residual pair Cb | Cr << 16; line_cb = the row
 // above the CTU in the Cb line buffer.
+template <typename T = uint8_t>
 __device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, uint32_t cw, uint32_t w0, uint32_t w1,
-                                             uint32_t w5, int r32, int lane, uint32_t tab) {
+                                             uint32_t w5, int r32, int lane, uint32_t tab, int maxv = 255) {
     constexpr int n = 8, ist = 32;
+    constexpr uint32_t PB = sizeof(T);
+    lbase /= PB; line_cb /= PB;                             // byte -> sample addresses (cw: samples)
     const int ofs = (int)(w0 & 0x1fffu);
     const int xr = (ofs - 4096) & 31, yr = (ofs - 4096) >> 5;
     const int mode = (int)((w0 >> 17) & 63u);
     const int k = min(lane, 4 * n);
     const int fa = (int)(w5 & 0xffu), la = (int)((w5 >> 8) & 0xffu);
     const int sref = min(max(k, fa), la);
-    const uint32_t orgA = lbase + kOrgC + (uint32_t)ofs;                            // Cb TB origin
-    const uint32_t lcolA = lbase + (uint32_t)offsetof(WaveLds, cleft) + (uint32_t)yr;
+    const uint32_t orgA = lbase + kOrgCT<T> + (uint32_t)ofs;                        // Cb TB origin
+    const uint32_t lcolA = lbase + kCLeftT<T> + (uint32_t)yr;
     const uint32_t lb = xr == 0 ? lcolA + 2 * n - 1 : orgA - 1 + (2 * n - 1) * ist;
     const int ls = xr == 0 ? 1 : ist;
     const uint32_t tb = (yr == 0 ? line_cb + (uint32_t)xr : orgA - ist) - 2 * n - 1;
@@ -771,18 +818,18 @@ __device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, u
     const bool left = sref < th;
     const uint32_t sa = tb + sref + (left ? (lb - tb) - (uint32_t)(sref * (ls + 1)) : 0u);
     const uint32_t dcr = left ? (xr == 0 ? 32u : 1024u) : (yr == 0 ? cw : 1024u);
-    const uint32_t cb = *lds8(sa), cr = *lds8(sa + dcr);
+    const uint32_t cb = *ldsT<T>(sa), cr = *ldsT<T>(sa + dcr);
     uint32_t te = w1;
     if constexpr (P265R_ANGTAB8) {                            // AngTab8 entry of sample lane
         te = *lds32(tab + (uint32_t)kAngTab4Bytes + (uint32_t)mode * 256u + (uint32_t)lane * 4u);
         asm volatile("" : "+v"(te));
     }
-    const uint32_t v = (w0 & J_NONE) ? 0x00800080u : (cb | cr << 16);
+    const uint32_t v = (w0 & J_NONE) ? (uint32_t)((maxv + 1) >> 1) * 0x00010001u : (cb | cr << 16);
     const int x = lane & 7, y = lane >> 3;
-    const uint32_t rec = cquad_recon(cpred<3, (bool)P265R_ANGTAB8>(mode, te, v, x, y, k), (uint32_t)r32);
+    const uint32_t rec = cquad_recon(cpred<3, (bool)P265R_ANGTAB8, T>(mode, te, v, x, y, k), (uint32_t)r32, maxv);
     const uint32_t da = orgA + (uint32_t)(y * ist + x);
-    *lds8(da) = (uint8_t)rec;
-    *lds8(da + 1024) = (uint8_t)(rec >> 16);
+    *ldsT<T>(da) = (T)(rec & 0xffffu);
+    *ldsT<T>(da + 1024) = (T)(rec >> 16);
     wave_sync();
 }
 
@@ -792,10 +839,9 @@ __device__ __forceinline__ void recon_cfast8(uint32_t lbase, uint32_t line_cb, u
 // reconstructed (rec: lane = region sample y * 8 + x); the source of every reference index is
 // a compile-time affine map per stage.  Lanes of sub-TB Q then predict (fast_pred) and
 // reconstruct their sample into rec.  CH: chroma quad, every value a packed Cb | Cr << 16 pair.
-template <int Q, bool CH>
+template <int Q, bool CH, typename T = uint8_t>
 __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, bool none, int fa, int la,
-                                          uint32_t te, int r16, int qid, int xs, int ys) {
-    constexpr int maxv = 255;
+                                          uint32_t te, int r16, int qid, int xs, int ys, int maxv = 255) {
     const int s = min(max(lane, fa), la);                        // substituted reference index
     auto bp = [](int i, int src) { return __builtin_amdgcn_ds_bpermute(i << 2, src); };
     int v;
@@ -813,12 +859,12 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     // only the first stage can find no reference available: stages 1-3 always have the region's earlier
     // sub-blocks (q1: q0's column on the left, q2: q0's row above, q3: both) -- their none bits are 0
     if constexpr (CH) {
-        if constexpr (Q == 0) v = none ? 0x00800080 : v;
-        const int rq = (int)cquad_recon(cpred<2, true>(mode, te, (uint32_t)v, xs, ys, lane), (uint32_t)r16);
+        if constexpr (Q == 0) v = none ? (int)((uint32_t)((maxv + 1) >> 1) * 0x00010001u) : v;
+        const int rq = (int)cquad_recon(cpred<2, true, T>(mode, te, (uint32_t)v, xs, ys, lane), (uint32_t)r16, maxv);
         return qid == Q ? rq : rec;
     } else {
-        if constexpr (Q == 0) v = none ? 128 : v;
-        const int rq = clip_pel(fast_pred<2, false, true>(mode, te, v, xs, ys, lane, lane, 0) + r16, maxv);
+        if constexpr (Q == 0) v = none ? (maxv + 1) >> 1 : v;
+        const int rq = clip_pel(fast_pred<2, false, true>(mode, te, v, xs, ys, lane, lane, 0, maxv) + r16, maxv);
         return qid == Q ? rq : rec;
     }
 }
@@ -831,14 +877,16 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
 // buffer, and pack them), the four stages pass their samples to each other through registers
 // (ds_bpermute), and the region is written to LDS once.  r16 = this lane's residual sample
 // (chroma: the packed Cb | Cr << 16 pair); line_top = the row above the CTU (chroma: the Cb line).
-template <bool CH>
+template <bool CH, typename T = uint8_t>
 __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t cw, uint32_t w0, uint32_t w1,
-                                           uint32_t w2, uint32_t tab, int r16, int lane) {
+                                           uint32_t w2, uint32_t tab, int r16, int lane, int maxv = 255) {
     constexpr int ist = CH ? 32 : 64, last = ist - 1;           // interior stride, last row / column
+    constexpr uint32_t PB = sizeof(T);
+    lbase /= PB; line_top /= PB;                                 // byte -> sample addresses (cw: samples)
     const int ofs = (int)(w0 & 0x1fffu);
     const int X = CH ? ((ofs - 4096) & 31) : (ofs & 63), Y = CH ? ((ofs - 4096) >> 5) : (ofs >> 6);
-    const uint32_t orgA = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs;
-    const uint32_t leftA = lbase + (uint32_t)(CH ? offsetof(WaveLds, cleft) : offsetof(WaveLds, yleft));
+    const uint32_t orgA = lbase + (CH ? kOrgCT<T> : kOrgLT<T>) + (uint32_t)ofs;
+    const uint32_t leftA = lbase + (CH ? kCLeftT<T> : kYLeftT<T>);
     // ---- external references: e = 0..12 column x = -1 (row e - 1), e = 13..24 row y = -1 ------
     const int e = min(CH ? (lane & 31) : lane, 24);
     // every candidate computed, then selected: no divergent branch per lane class
@@ -847,10 +895,10 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     const uint32_t col = X > 0 ? orgA - 1 + (uint32_t)((r - Y) * ist) : leftA + (uint32_t)r;
     const uint32_t row = Y == 0 ? line_top + (uint32_t)(X + c) : orgA - ist + (uint32_t)min(c, last - X);
     const uint32_t ea = e > 12 ? row : (r < 0 ? line_top + (uint32_t)(X - 1) : col);
-    int ext = (int)*lds8(ea);
+    int ext = (int)*ldsT<T>(ea);
     if constexpr (CH) {                                          // Cb | Cr << 16 (same LDS round trip)
         const uint32_t dcr = e > 12 ? (Y == 0 ? cw : 1024u) : (r < 0 ? cw : (X > 0 ? 1024u : 32u));
-        ext |= (int)*lds8(ea + dcr) << 16;
+        ext |= (int)*ldsT<T>(ea + dcr) << 16;
     }
     const int xs = lane & 3, ys = (lane >> 3) & 3;
     const int qid = ((lane >> 4) & 2) | ((lane >> 2) & 1);
@@ -862,31 +910,31 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     P265R_MARK("quad_stage0");
     {
         const uint32_t m = (w0 >> 17) & 63u;
-        rec = quad_stage<0, CH>(rec, ext, lane, (int)m, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
-                                ang(m), r16, qid, xs, ys);
+        rec = quad_stage<0, CH, T>(rec, ext, lane, (int)m, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
+                                   ang(m), r16, qid, xs, ys, maxv);
     }
     P265R_MARK("quad_stage1");
     {
         const uint32_t m = (w0 >> 23) & 63u;
-        rec = quad_stage<1, CH>(rec, ext, lane, (int)m, (w0 >> 30) & 1u, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
-                                ang(m), r16, qid, xs, ys);
+        rec = quad_stage<1, CH, T>(rec, ext, lane, (int)m, (w0 >> 30) & 1u, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
+                                   ang(m), r16, qid, xs, ys, maxv);
     }
     P265R_MARK("quad_stage2");
     {
         const uint32_t m = w1 & 63u;
-        rec = quad_stage<2, CH>(rec, ext, lane, (int)m, (w1 >> 12) & 1u, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
-                                ang(m), r16, qid, xs, ys);
+        rec = quad_stage<2, CH, T>(rec, ext, lane, (int)m, (w1 >> 12) & 1u, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
+                                   ang(m), r16, qid, xs, ys, maxv);
     }
     P265R_MARK("quad_stage3");
     {
         const uint32_t m = (w1 >> 6) & 63u;
-        rec = quad_stage<3, CH>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
-                                ang(m), r16, qid, xs, ys);
+        rec = quad_stage<3, CH, T>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
+                                   ang(m), r16, qid, xs, ys, maxv);
     }
     P265R_MARK("quad_store");
-    const uint32_t da = lbase + (CH ? kOrgC : kOrgL) + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
-    *lds8(da) = (uint8_t)rec;
-    if constexpr (CH) *lds8(da + 1024) = (uint8_t)(rec >> 16);
+    const uint32_t da = lbase + (CH ? kOrgCT<T> : kOrgLT<T>) + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
+    *ldsT<T>(da) = (T)((uint32_t)rec & 0xffffu);
+    if constexpr (CH) *ldsT<T>(da + 1024) = (T)((uint32_t)rec >> 16);
     wave_sync();
 }
 
@@ -912,7 +960,7 @@ struct XgBuf {
     int xg, seq;                 // workgroups per chain; this run's tag
 };
 
-template <int W, int WPE, bool XG = false, bool TRCHK = false>
+template <int W, int WPE, bool XG = false, bool TRCHK = false, typename T = uint8_t>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
 void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                            const int16_t* __restrict__ pool,
@@ -926,6 +974,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #else
 #define P265R_TRACE(code) do { } while (0)
 #endif
+    static_assert(sizeof(T) == 1 || !XG, "the cross-group layout is 8-bit only");
+    constexpr int PB = (int)sizeof(T);                // bytes per sample
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     RowCtrl& ctl = *reinterpret_cast<RowCtrl*>(smem);
     const int wave = threadIdx.x >> 6;
@@ -936,9 +986,10 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
     // progress words: one per (slot, CTU row, component) in either mode (host: launch_rows_w lds_of)
     const int prog_bytes = (fs_count * 2 * g.hc * 4 + 15) & ~15;
     int* prog = reinterpret_cast<int*>(smem + 256);
-    WaveLds& L = reinterpret_cast<WaveLds*>(smem + 256 + prog_bytes)[wave];
-    const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows
-    unsigned char* lines = smem + 256 + prog_bytes + W * sizeof(WaveLds);
+    WaveLdsT<T>& L = reinterpret_cast<WaveLdsT<T>*>(smem + 256 + prog_bytes)[wave];
+    const int line_bytes = g.w + 2 * g.cw;            // Y | Cb | Cr bottom sample rows (samples)
+    T* lines = reinterpret_cast<T*>(smem + 256 + prog_bytes + W * sizeof(WaveLdsT<T>));
+    const int maxv = (1 << g.bd[0]) - 1;              // BitDepth: luma = chroma (p265r_create)
 
     uint32_t* const atab = reinterpret_cast<uint32_t*>(lines + (size_t)fs_count * 2 * line_bytes);   // AngTab4
     if (threadIdx.x == 0) {
@@ -1073,8 +1124,8 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             __hip_atomic_fetch_add(&ctl.done[slot], lane == 0 ? 1 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             continue;
         }
-        unsigned char* line_cur = lines + (size_t)(slot * 2 + (cy & 1)) * line_bytes;
-        const unsigned char* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
+        T* line_cur = lines + (size_t)(slot * 2 + (cy & 1)) * line_bytes;
+        const T* line_up = lines + (size_t)(slot * 2 + ((cy & 1) ^ 1)) * line_bytes;
         int* my_prog = &prog[(slot * g.hc + cy) * 2 + comp];
         const int* up_prog = &prog[(slot * g.hc + (cy > 0 ? cy - 1 : 0)) * 2 + comp];
         const int tag = ((XG ? xb.seq : j) & 0xffff) << 16;
@@ -1165,7 +1216,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                                                       (size_t)h * (xg_row_bytes >> 1) + cts + (x0 >> comp) - 4 + 4 * k;
                     const uint32_t v = __hip_atomic_load(reinterpret_cast<const P265R_GLOBAL uint32_t*>(src),
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    uint8_t* dst = comp ? &L.ctop[h][4 * k] : &L.ytop[4 * k];
+                    T* dst = comp ? &L.ctop[h][4 * k] : &L.ytop[4 * k];
                     *reinterpret_cast<uint32_t*>(dst) = v;
                 }
                 wave_sync();
@@ -1177,7 +1228,7 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int h = comp ? lane >> 5 : 0, k = comp ? lane & 31 : lane;
                 const int hv = min(cts, (comp ? ph >> 1 : ph) - (y0 >> comp));
                 if (k < nd) {
-                    const uint8_t* src = (comp ? L.c[h] : L.y) + (hv - 1) * (comp ? 32 : 64) + 4 * k;
+                    const T* src = (comp ? L.c[h] : L.y) + (hv - 1) * (comp ? 32 : 64) + 4 * k;
                     P265R_GLOBAL uint8_t* dl = xg_line + (size_t)cy * xg_row_bytes + (size_t)h * (xg_row_bytes >> 1) +
                                                cts + (x0 >> comp) + 4 * k;
                     __hip_atomic_store(reinterpret_cast<P265R_GLOBAL uint32_t*>(dl), *reinterpret_cast<const uint32_t*>(src),
@@ -1206,10 +1257,10 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
             P265R_TRACE(4 | (cx << 8) | (r << 16));
             const IntraJob* jl = jobs + tb_begin + (comp ? 0 : n_chroma);
             // line buffer row above, per lane component (pair jobs: lanes 32-63 are Cr); XG: the wave's copy
-            const uint8_t* ltop_l = XG ? &L.ytop[4] : line_up + x0;
-            const uint8_t* ltop_c = XG ? &L.ctop[lane >> 5][4] : line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
-            const uint8_t* ltop_cb = XG ? &L.ctop[0][4] : line_up + g.w + (x0 >> 1);
-            const uint32_t cr_off = XG ? (uint32_t)sizeof(L.ctop[0]) : (uint32_t)g.cw;   // Cb -> Cr in the row above
+            const T* ltop_l = XG ? &L.ytop[4] : line_up + x0;
+            const T* ltop_c = XG ? &L.ctop[lane >> 5][4] : line_up + g.w + (lane >> 5) * g.cw + (x0 >> 1);
+            const T* ltop_cb = XG ? &L.ctop[0][4] : line_up + g.w + (x0 >> 1);
+            const uint32_t cr_off = XG ? (uint32_t)(sizeof(L.ctop[0]) / PB) : (uint32_t)g.cw;   // Cb -> Cr in the row above (samples)
 
             // residual of job t: two aligned 16-B loads per lane (fixed shape, pools padded
             // by 64 B), issued while job t-1 is processed.  TB offsets are multiples of 16.
@@ -1365,31 +1416,33 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
 #endif
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"((uint32_t)(uintptr_t)ltop_l));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(tc) : "v"((uint32_t)(uintptr_t)ltop_c));
-                WaveLds& LL = *reinterpret_cast<WaveLds*>(lds_ptr(lbase));
-                const uint8_t* tlp = reinterpret_cast<const uint8_t*>(lds_ptr(tl));
-                const uint8_t* tcp = reinterpret_cast<const uint8_t*>(lds_ptr(tc));
+                WaveLdsT<T>& LL = *reinterpret_cast<WaveLdsT<T>*>(lds_ptr(lbase));
+                const T* tlp = reinterpret_cast<const T*>(lds_ptr(tl));
+                const T* tcp = reinterpret_cast<const T*>(lds_ptr(tc));
+                // (8 bits: the constant 255 folds into every job function, as before the 16-bit path)
+                const int mv = PB == 1 ? 255 : maxv;
                 if (w5 & J5_QUAD) {
-                    if ((w0 >> 15) & 3u) recon_quad<true>(lbase, tcb, cr_off, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln);
-                    else recon_quad<false>(lbase, tl, 0u, w0, w1, w2, tab, c16, ln);
+                    if ((w0 >> 15) & 3u) recon_quad<true, T>(lbase, tcb, cr_off, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, mv);
+                    else recon_quad<false, T>(lbase, tl, 0u, w0, w1, w2, tab, c16, ln, mv);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
-                        case 0: recon_fast<2, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;
-                        case 1: recon_fast<3, false>(lbase, tl, w0, w1, w5, c16, ln, tab); break;
-                        case 2: recon_fast16(lbase, tl, w0, w1, w5, make_uint4((uint32_t)c16, (uint32_t)c16m, 0u, 0u), ln); break;
-                        case 5: recon_cfast8(lbase, tcb, cr_off, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, tab); break;
-                        default: recon_fast<2, true>(lbase, tc, w0, w1, w5, c16, ln, tab); break;
+                        case 0: recon_fast<2, false, T>(lbase, tl, w0, w1, w5, c16, ln, tab, mv); break;
+                        case 1: recon_fast<3, false, T>(lbase, tl, w0, w1, w5, c16, ln, tab, mv); break;
+                        case 2: recon_fast16<T>(lbase, tl, w0, w1, w5, make_uint4((uint32_t)c16, (uint32_t)c16m, 0u, 0u), ln, mv); break;
+                        case 5: recon_cfast8<T>(lbase, tcb, cr_off, w0, w1, w5, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, tab, mv); break;
+                        default: recon_fast<2, true, T>(lbase, tc, w0, w1, w5, c16, ln, tab, mv); break;
                     }
                 } else {
                   const uint4* ra_p = res_addr(w0, w3, w4);
                   const uint4 ca = ld16(ra_p), cb = ld16(ra_p + 1);
                   switch (sel) {
-                    case 0: recon_job<2, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
-                    case 1: recon_job<3, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
-                    case 2: recon_job<4, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
-                    case 3: recon_job<5, false>(LL, tlp, w0, w1, w2, ca, cb, ln); break;
-                    case 4: recon_job<2, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
-                    case 5: recon_job<3, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
-                    default: recon_job<4, true>(LL, tcp, w0, w1, w2, ca, cb, ln); break;
+                    case 0: recon_job<2, false, T>(LL, tlp, w0, w1, w2, ca, cb, ln, mv); break;
+                    case 1: recon_job<3, false, T>(LL, tlp, w0, w1, w2, ca, cb, ln, mv); break;
+                    case 2: recon_job<4, false, T>(LL, tlp, w0, w1, w2, ca, cb, ln, mv); break;
+                    case 3: recon_job<5, false, T>(LL, tlp, w0, w1, w2, ca, cb, ln, mv); break;
+                    case 4: recon_job<2, true, T>(LL, tcp, w0, w1, w2, ca, cb, ln, mv); break;
+                    case 5: recon_job<3, true, T>(LL, tcp, w0, w1, w2, ca, cb, ln, mv); break;
+                    default: recon_job<4, true, T>(LL, tcp, w0, w1, w2, ca, cb, ln, mv); break;
                   }
                 }
                 P265R_MARK("job_end");
@@ -1434,28 +1487,29 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 const int Wd = c ? pw >> 1 : pw, Ht = c ? ph >> 1 : ph;
                 const int xb = x0 >> sub, yb = y0 >> sub;
                 const int wv = min(cs, Wd - xb), hv = min(cs, Ht - yb);
-                const uint8_t* src = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
+                const T* src = c == 0 ? L.y : (c == 1 ? L.c[0] : L.c[1]);
                 const int ist = c ? 32 : 64;
-                P265R_GLOBAL uint8_t* plane = gptr_w(uniform(gload(&Pp->rec[c])));
-                const int st = (c ? g.stride[1] : g.stride[0]);
-                if (cs >= 16) {
-                    // 2^lg 16-sample chunks per CTB row (one ds_read_b128 + one 16-B global store per
+                P265R_GLOBAL T* plane = reinterpret_cast<P265R_GLOBAL T*>(gptr_w(uniform(gload(&Pp->rec[c]))));
+                const int st = (c ? g.stride[1] : g.stride[0]);      // samples
+                constexpr int LC = PB == 1 ? 4 : 3;                    // log2 samples per 16-B chunk
+                if (cs * PB >= 16) {
+                    // 2^lg 16-B chunks per CTB row (one ds_read_b128 + one 16-B global store per
                     // lane and chunk).  A chunk that straddles the picture's right edge is stored whole:
                     // the plane rows are padded to 64 B (stride >= xb + cs), and nothing reads the
                     // padding (downloads copy the width, SAO / deblocking clamp to it)
-                    const int lg = g.ctb_log2 - sub - 4;
+                    const int lg = g.ctb_log2 - sub - LC;
                     for (int e = lane; e < (hv << lg); e += 64) {
-                        const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << 4;
+                        const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << LC;
                         if (xx < wv)
                             *reinterpret_cast<P265R_GLOBAL u32x4_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
                                 *reinterpret_cast<const u32x4_t*>(src + yy * ist + xx);
                     }
                 } else {
-                    // 2^lg words (4 samples) per CTB row, no per-word division; the words past a
+                    // 2^lg words (4 bytes) per CTB row, no per-word division; the words past a
                     // picture's right edge idle
-                    const int lg = g.ctb_log2 - sub - 2;
+                    const int lg = g.ctb_log2 - sub - (LC - 2);
                     for (int e = lane; e < (hv << lg); e += 64) {
-                        const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << 2;
+                        const int yy = e >> lg, xx = (e & ((1 << lg) - 1)) << (LC - 2);
                         if (xx < wv)
                             *reinterpret_cast<P265R_GLOBAL uint32_t*>(plane + (size_t)(yb + yy) * st + xb + xx) =
                                 *reinterpret_cast<const uint32_t*>(src + yy * ist + xx);
@@ -1469,10 +1523,10 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                                            *reinterpret_cast<const uint32_t*>(src + (hv - 1) * ist + 4 * lane),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } else {
-                    unsigned char* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
+                    T* lc = line_cur + (c == 0 ? 0 : (c == 1 ? g.w : g.w + g.cw)) + xb;
                     if (lane < wv) lc[lane] = src[(hv - 1) * ist + lane];
                 }
-                uint8_t* lf = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
+                T* lf = c == 0 ? L.yleft : (c == 1 ? L.cleft[0] : L.cleft[1]);
                 if (lane < hv) lf[lane] = src[lane * ist + wv - 1];
             }
             if constexpr (XG) {

@@ -28,6 +28,7 @@
 #include "intra_rows.h"
 #include "loopfilter.h"
 #include "loopfilter16.h"
+#include "sao16.h"
 #include "residual.h"
 #include "sao.h"
 #include "sao_strip16.h"
@@ -367,19 +368,23 @@ int join_sao(p265r_batch* b) {
     return P265R_OK;
 }
 
-template <int W, int WPE, bool XG = false, bool TRCHK = false>
+// dynamic LDS of the row kernel with W waves and f picture slots (launch_rows_w)
+template <typename T>
+size_t rows_lds_bytes(const Geo& g, int W, int f) {
+    return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLdsT<T>) +
+           (size_t)f * 2 * (g.w + 2 * g.cw) * sizeof(T) + kAngTabBytes;
+}
+
+template <int W, int WPE, bool XG = false, bool TRCHK = false, typename T = uint8_t>
 int launch_rows_w(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     Geo g = ctx->geo;
     // picture slots: the W rows in flight are consecutive in the queue, so they span at
     // most ceil(W / hc) + 1 pictures; a slot is reused only after its previous picture is
     // complete (the kernel waits for that, so fewer slots would still be correct)
     int fs = std::min(32, (W + 2 * g.hc - 1) / (2 * g.hc) + 1);     // 2 row units (luma, chroma) per CTU row
-    auto lds_of = [&](int f) {
-        return 256 + (size_t)((f * 2 * g.hc * 4 + 15) & ~15) + W * sizeof(WaveLds) + (size_t)f * 2 * (g.w + 2 * g.cw) +
-               kAngTabBytes;
-    };
+    auto lds_of = [&](int f) { return rows_lds_bytes<T>(g, W, f); };
     while (fs > 2 && lds_of(fs) > 160 * 1024) --fs;
-    auto fn = intra_rows_kernel<W, WPE, XG, TRCHK>;
+    auto fn = intra_rows_kernel<W, WPE, XG, TRCHK, T>;
     bool split = false;
     {
         // every workgroup resident at once and holding a single picture: one slot is enough
@@ -458,6 +463,16 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     // tile units, the decoder's small batches): W = 16, so every CTU row of a picture's chain can
     // be in flight at once (a 2-CTU-lag wavefront of 17 rows needs 17 waves; with 12 the rows
     // after the 12th wait for a whole row to finish)
+    // 16-bit samples (BitDepth 9..10): the same row pipeline on uint16_t LDS tiles and line buffers
+    // (one workgroup per CU: twice the LDS of a wave); W = 12 alone, W = 8 beside other lanes' work
+    if (ctx->geo.pel16) {
+        // (wide pictures: W = 12 only while its two picture slots fit the 160 KB of LDS; p265r_create keeps
+        // the per-diagonal schedule for pictures too wide for W = 8)
+        int w = ctx->row_waves ? ctx->row_waves : (alone ? 12 : 8);
+        if (w == 12 && rows_lds_bytes<uint16_t>(ctx->geo, 12, 2) > 160 * 1024) w = 8;
+        return w == 12 ? launch_rows_w<12, 1, false, false, uint16_t>(ctx, b, st, alone)
+                       : launch_rows_w<8, 1, false, false, uint16_t>(ctx, b, st, alone);
+    }
     // smaller still (every chain on xg CUs of its own): the cross-group kernel, one wave per SIMD
     if (ctx->row_waves == 0 && b->d_xg_prog && 2 * (long long)b->n_pics * ctx->xg <= ctx->num_cus)
         return ctx->geo.tr_check ? launch_rows_w<4, 1, true, true>(ctx, b, st, alone)     // (test build of it)
@@ -541,7 +556,9 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
                           "P265R_FORK_PREP", "P265R_SPLIT", "P265R_XG", "P265R_TR_CHECK"})
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
-    if (g.pel16) ctx->schedule = 0;          // 16-bit samples: the per-diagonal intra kernel
+    // 16-bit samples: the row pipeline while a W = 8 workgroup's LDS tiles and two line-buffer slots fit
+    // 160 KB (pictures up to ≈ 4K wide), else the per-diagonal kernel
+    if (g.pel16 && rows_lds_bytes<uint16_t>(g, 8, 2) > 160 * 1024) ctx->schedule = 0;
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';
@@ -1154,7 +1171,14 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         s = ctx->aux[li];
         HIP_TRY(hipStreamWaitEvent(s, b->intra_done, 0));
     }
-    if (g.pel16 && (b->dbk || b->sao) && !(skip & 4)) {
+    if (g.pel16 && b->sao && !b->dbk && !(skip & 4)) {
+        // 16-bit samples, SAO only: the streaming kernel (sao16.h), 8 samples per thread, XCD-aware blocks
+        const long long blocks = (long long)sao16_rows(g) * b->n_pics;
+        if (blocks >= (1ll << 31) - 8) return P265R_ERANGE;
+        sao16_kernel<<<(unsigned)((blocks + 7) / 8 * 8), 256, 0, s>>>(b->d_pics, g, b->n_pics);
+        ++tm.sao_launches;
+        HIP_TRY(hipGetLastError());
+    } else if (g.pel16 && (b->dbk || b->sao) && !(skip & 4)) {
         // 16-bit samples (Main 10): deblocking + SAO in loopfilter16.h, with or without deblocking
         const long long units = (long long)ctx->n_ctus * b->n_pics;
         if (units >= (1ll << 31) - 8) return P265R_ERANGE;

@@ -1,6 +1,7 @@
 """Main 10 (BitDepth 10) on the GPU through the C ABI vs the oracles, bit-exact.
 
-The 16-bit sample path (uint16_t planes; per-diagonal intra kernel intra_step_kernel<uint16_t>,
+The 16-bit sample path (uint16_t planes; the row pipeline on uint16_t LDS tiles, intra_rows_kernel<..., uint16_t>,
+and the per-diagonal kernel intra_step_kernel<uint16_t> (P265R_SCHEDULE=steps); sao16.h for SAO-only batches,
 loopfilter16.h; the residual kernels with bdShift = BitDepth + log2 - 5 and 20 - BitDepth) against
 oracle/recon_oracle.py (pinned at 10 bits by tests/golden/ref_components_bd10.npz from the reference's
 own scaling / prediction / reconstruction, tests/test_oracle_vs_reference.py) and its C twin.
@@ -50,11 +51,16 @@ def test_main10_uniform_modes(recon_mod, ctb_log2, w, h, deblocking):
     _check(recon_mod, params, pics, "main10 uniform")
 
 
-def test_main10_slices_tiles_pcm_bypass_tskip(recon_mod):
-    params = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, loop_filter_across_tiles=0,
+@pytest.mark.parametrize("deblocking", ["random", False])
+@pytest.mark.parametrize("ctb_log2,lf_tiles", [(5, 0), (4, 1), (6, 0)])
+def test_main10_slices_tiles_pcm_bypass_tskip(recon_mod, deblocking, ctb_log2, lf_tiles):
+    """Slices (with and without loop filtering across them), tiles, PCM, bypass, transform skip; without
+    deblocking the batch takes the streaming SAO kernel (sao16.h), with it loopfilter16.h."""
+    params = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=ctb_log2, loop_filter_across_tiles=lf_tiles,
                            bit_depth_luma=10, bit_depth_chroma=10)
-    pics = [synth.make_picture(params, 5200 + s, perf=False, tiles=(3, 2), n_slices=4, lf_across_slices=None,
-                               deblocking="random", bypass_rate=0.05, pcm_rate=0.03, tskip_rate=0.3) for s in range(2)]
+    pics = [synth.make_picture(params, 5200 + s + 10 * ctb_log2, perf=False, tiles=(3, 2), n_slices=4,
+                               lf_across_slices=None, deblocking=deblocking, bypass_rate=0.05, pcm_rate=0.03,
+                               tskip_rate=0.3) for s in range(2)]
     _check(recon_mod, params, pics, "main10 tiles")
 
 
@@ -77,7 +83,8 @@ def test_main10_9bit(recon_mod):
     _check(recon_mod, params, pics, "9-bit")
 
 
-def test_main10_ragged_batch_and_digest(recon_mod):
+@pytest.mark.parametrize("deblocking", [True, False])
+def test_main10_ragged_batch_and_digest(recon_mod, deblocking):
     """A ragged 10-bit batch (four picture sizes) and the device digest of uint16 planes (32-bit words of two
     samples) equal the host digest of the oracle's planes."""
     big = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, bit_depth_luma=10, bit_depth_chroma=10)
@@ -85,7 +92,7 @@ def test_main10_ragged_batch_and_digest(recon_mod):
     pics = []
     for k, (w, h) in enumerate(sizes):
         pp = R.pic_params(big, R.Picture(ctus=None, tbs=None, coef=None, size=(w, h)))
-        pic = synth.make_picture(pp, 5600 + k, perf=bool(k % 2), deblocking=True)
+        pic = synth.make_picture(pp, 5600 + k, perf=bool(k % 2), deblocking=deblocking)
         pic.size = (w, h)
         pics.append(pic)
     _check(recon_mod, big, pics, "main10 ragged")
@@ -98,6 +105,36 @@ def test_main10_ragged_batch_and_digest(recon_mod):
         rec_ref, out_ref = O.decode_picture(R.params_dict(R.pic_params(big, pic)), pic.as_oracle_dict())
         assert np.array_equal(got[i], digest.picture_digest([np.asarray(p, np.uint16) for p in out_ref])), "out %d" % i
         assert np.array_equal(got_rec[i], digest.picture_digest([np.asarray(p, np.uint16) for p in rec_ref])), "rec %d" % i
+
+
+def test_main10_row_pipeline_and_schedules(recon_mod, monkeypatch):
+    """The 16-bit row pipeline (W = 12 alone, W = 8 while another lane runs, the component split of a small
+    batch) and the per-diagonal schedule (P265R_SCHEDULE=steps) give the same planes."""
+    params = R.make_params(pic_width=352, pic_height=288, bit_depth_luma=10, bit_depth_chroma=10)
+    pics = [synth.make_picture(params, 5700 + s, perf=bool(s % 2), deblocking=bool(s % 3 == 0), tskip_rate=0.2)
+            for s in range(6)]
+    ref = _check(recon_mod, params, pics, "main10 rows")
+    with recon_mod.ReconContext(params) as ctx:
+        ctx.set_pipeline(2)
+        ba, bb = ctx.upload(pics[:3]), ctx.upload(pics[3:])
+        for _ in range(2):
+            ctx.run(ba)
+            ctx.run(bb)
+        ctx.sync()
+        outs = ctx.download(ba) + ctx.download(bb)
+        d = ctx.describe()
+        ba.free(); bb.free()
+    assert d["schedule"] == "rows"
+    for i in range(6):
+        for c in range(3):
+            np.testing.assert_array_equal(outs[i][c], ref[i][c], err_msg="pipelined pic %d c%d" % (i, c))
+    monkeypatch.setenv("P265R_SCHEDULE", "steps")
+    with recon_mod.ReconContext(params) as ctx:
+        assert ctx.describe()["schedule"] == "steps"
+        outs = ctx.decode(pics)
+    for i in range(6):
+        for c in range(3):
+            np.testing.assert_array_equal(outs[i][c], ref[i][c], err_msg="steps pic %d c%d" % (i, c))
 
 
 def test_unsupported_bit_depths_rejected(recon_mod):
