@@ -1172,10 +1172,12 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
         HIP_TRY(hipStreamWaitEvent(s, b->intra_done, 0));
     }
     if (g.pel16 && b->sao && !b->dbk && !(skip & 4)) {
-        // 16-bit samples, SAO only: the streaming kernel (sao16.h), 8 samples per thread, XCD-aware blocks
-        const long long blocks = (long long)sao16_rows(g) * b->n_pics;
-        if (blocks >= (1ll << 31) - 8) return P265R_ERANGE;
-        sao16_kernel<<<(unsigned)((blocks + 7) / 8 * 8), 256, 0, s>>>(b->d_pics, g, b->n_pics);
+        // 16-bit samples, SAO only: the strip kernel (sao16.h), 8 samples per lane, one wave per (picture,
+        // CTB row, component, 496-sample strip), 4 waves per block, blocks dealt XCD-aware
+        const long long waves = (long long)sao16b_units(g) * b->n_pics;
+        if (waves >= (1ll << 31) - 64) return P265R_ERANGE;
+        const unsigned blocks = (unsigned)((waves + 3) / 4 + 7) / 8 * 8;
+        sao16_strip_kernel<<<blocks, 256, 0, s>>>(b->d_pics, g, b->view, b->n_pics);
         ++tm.sao_launches;
         HIP_TRY(hipGetLastError());
     } else if (g.pel16 && (b->dbk || b->sao) && !(skip & 4)) {
