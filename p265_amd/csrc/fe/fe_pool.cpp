@@ -14,7 +14,7 @@ namespace {
 
 constexpr size_t kHeader = 64;                 // block header: capacity (keeps 64-B data alignment)
 constexpr size_t kPoolMin = 256u << 10;        // smaller blocks go straight back to malloc
-constexpr size_t kPoolCap = 1024ull << 20;     // idle bytes kept at most
+constexpr size_t kPoolCap = 2048ull << 20;     // idle bytes kept at most (≈200 1080p pictures)
 
 struct Pool {
     std::mutex mu;

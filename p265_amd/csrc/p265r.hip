@@ -854,7 +854,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
             nf += pics[i].nofilter ? 1 : 0;
         }
     }
-    parallel_for(n_pics, [&](int i) {
+    auto pack_pic = [&](int i) {
         const p265r_picture& pic = pics[i];
         std::memcpy(h_ctus + (size_t)i * nc, pic.ctus, sizeof(p265r_ctu) * pnc[i]);
         if (pnc[i] < nc) std::memset(h_ctus + (size_t)i * nc + pnc[i], 0, sizeof(p265r_ctu) * (nc - pnc[i]));
@@ -903,7 +903,39 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         } else {
             dp.nofilter = nullptr;
         }
-    });
+        };
+    // Packing and H2D overlap: the pictures go in chunks; a chunk's ranges of every array (CTU and TB
+    // records, each class slab of the coefficient pool, each residual job list, no-filter maps) are
+    // enqueued as soon as the chunk is packed, so the DMA engine copies chunk k while the host packs
+    // chunk k + 1 (the staging ranges of different chunks are disjoint).  The DevPic table and the
+    // error word follow last; the gaps between the arrays are zeroed on the device.
+    (void)hipSetDevice(ctx->device);
+    if (P265R_UP_STREAM == 2 && !ctx->up_stream && e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
+    hipStream_t st = P265R_UP_STREAM ? ctx->up_stream : b->stream;
+    auto h2d = [&](size_t dev_off, size_t host_off, size_t bytes) {
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(dbase + dev_off, host + host_off, bytes, hipMemcpyHostToDevice, st);
+    };
+    if (e == hipSuccess) e = hipMemsetAsync(dbase + o_res, 0, o_ijobs - o_res, st);   // residual pool, job lists
+    if (e == hipSuccess) e = hipMemsetAsync(dbase + o_ijobs, 0, o_rec - o_ijobs, st);
+    const int n_chunks = std::max(1, std::min(n_pics / 8, 4));
+    for (int k = 0; k < n_chunks; ++k) {
+        const int p0 = (int)((long long)n_pics * k / n_chunks), p1 = (int)((long long)n_pics * (k + 1) / n_chunks);
+        parallel_for(p1 - p0, [&](int j) { pack_pic(p0 + j); });
+        h2d(o_ctus + sizeof(p265r_ctu) * nc * (size_t)p0, o_ctus + sizeof(p265r_ctu) * nc * (size_t)p0,
+            sizeof(p265r_ctu) * nc * (size_t)(p1 - p0));
+        const size_t t1 = p1 < n_pics ? tb_at[p1] : n_tbs_total;
+        h2d(o_tbs + sizeof(p265r_tb) * tb_at[p0], o_tbs + sizeof(p265r_tb) * tb_at[p0], sizeof(p265r_tb) * (t1 - tb_at[p0]));
+        for (int c = 0; c < N_POOLS; ++c) {
+            const size_t q0 = pool_at[p0][c], q1 = p1 < n_pics ? pool_at[p1][c] : pool_base[c] + pool_sz[c];
+            h2d(o_pool + sizeof(int16_t) * q0, o_pool + sizeof(int16_t) * q0, sizeof(int16_t) * (q1 - q0));
+        }
+        for (int c = 0; c < RC_NUM; ++c) {
+            const size_t j0 = (size_t)job_at[p0][c], j1 = p1 < n_pics ? (size_t)job_at[p1][c] : (size_t)n_jobs[c];
+            h2d(o_jobs[c] + sizeof(ResJob) * j0, s_jobs + (o_jobs[c] - o_jobs[0]) + sizeof(ResJob) * j0, sizeof(ResJob) * (j1 - j0));
+        }
+        const size_t f1 = p1 < n_pics ? nf_at[p1] : n_nf;
+        h2d(o_nf + nf_bytes * nf_at[p0], s_nf + nf_bytes * nf_at[p0], nf_bytes * (f1 - nf_at[p0]));
+    }
     P265R_UT("pack");
     std::memcpy(host + o_pics, b->h_pics.data(), sizeof(DevPic) * n_pics);
     b->view.rec0 = dbase + o_rec;
@@ -915,31 +947,19 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     b->view.ctus0 = reinterpret_cast<const p265r_ctu*>(dbase + o_ctus);
     b->view.err = b->d_err;
     std::memset(host + o_err, 0, o_ctus - o_err);                                        // error word
-    // alignment gaps between the arrays: zero, as the device image always had them
+    std::memset(host + o_pics + sizeof(DevPic) * n_pics, 0, o_err - (o_pics + sizeof(DevPic) * n_pics));
+    // alignment gaps between the arrays and the coefficient pool's pad: zero on the device, as the device
+    // image always had them; then the DevPic table and the error word (complete before returning: the
+    // staging buffer is refilled by the next upload)
     {
-        const size_t pics_end = o_pics + sizeof(DevPic) * n_pics;
         const size_t ctus_end = o_ctus + sizeof(p265r_ctu) * nc * (size_t)n_pics;
         const size_t tbs_end = o_tbs + sizeof(p265r_tb) * n_tbs_total;
-        std::memset(host + pics_end, 0, o_err - pics_end);
-        std::memset(host + ctus_end, 0, o_tbs - ctus_end);
-        std::memset(host + tbs_end, 0, o_pool - tbs_end);
-        for (int c = 0; c < RC_NUM; ++c) {
-            const size_t je = o_jobs[c] + sizeof(ResJob) * n_jobs[c];
-            const size_t next_start = c + 1 < RC_NUM ? o_jobs[c + 1] : o_ijobs;
-            std::memset(host + s_jobs + (je - o_jobs[0]), 0, next_start - je);
-        }
+        const size_t pool_end = o_pool + sizeof(int16_t) * pool_total;
+        if (e == hipSuccess && o_tbs > ctus_end) e = hipMemsetAsync(dbase + ctus_end, 0, o_tbs - ctus_end, st);
+        if (e == hipSuccess && o_pool > tbs_end) e = hipMemsetAsync(dbase + tbs_end, 0, o_pool - tbs_end, st);
+        if (e == hipSuccess && o_res > pool_end) e = hipMemsetAsync(dbase + pool_end, 0, o_res - pool_end, st);
     }
-    std::memset(host + o_pool + sizeof(int16_t) * pool_total, 0, o_res - o_pool - sizeof(int16_t) * pool_total);  // pool pad
-    // device image: host-filled ranges copied, everything else of [0, o_rec) zero, on the upload
-    // stream (a reused allocation's previous batch completed before p265r_batch_free returned);
-    // complete before returning (the staging buffer is refilled by the next upload)
-    if (P265R_UP_STREAM == 2 && !ctx->up_stream && e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking);
-    hipStream_t st = P265R_UP_STREAM ? ctx->up_stream : b->stream;
-    e = hipMemcpyAsync(dbase, host, o_res, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemsetAsync(dbase + o_res, 0, o_jobs[0] - o_res, st);
-    if (e == hipSuccess && jobs_bytes) e = hipMemcpyAsync(dbase + o_jobs[0], host + s_jobs, jobs_bytes, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemsetAsync(dbase + o_ijobs, 0, o_rec - o_ijobs, st);
-    if (e == hipSuccess && n_nf) e = hipMemcpyAsync(dbase + o_nf, host + s_nf, nf_bytes * n_nf, hipMemcpyHostToDevice, st);
+    h2d(0, 0, o_ctus);
     if (e == hipSuccess && recon_input) {
         for (int i = 0; i < n_pics && e == hipSuccess; ++i)
             for (int c = 0; c < 3 && e == hipSuccess; ++c) {

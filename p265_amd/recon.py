@@ -169,14 +169,27 @@ class ReconContext:
     def run(self, batch):
         _lib.check(self.lib.p265r_batch_run(self.handle, batch.handle), "p265r_batch_run")
 
-    def download(self, batch, with_recon=False, only=None):
+    def download(self, batch, with_recon=False, only=None, into=None):
         """Planes of the batch's pictures (after its last run).  ``only``: indices of the pictures
-        to copy back (the others are not transferred and come back as None)."""
+        to copy back (the others are not transferred and come back as None).  ``into``: the output
+        planes to fill instead of new arrays (a frame pool: per picture three C-contiguous arrays of the
+        planes' shapes and dtype, e.g. a previous download's result) -- fresh host memory costs a page
+        fault per 4 KB on its first write."""
         n = len(batch.pics)
         sel = set(range(n)) if only is None else {int(i) for i in only}
         shp = [plane_shapes(R.pic_params(self.params, p)) for p in batch.pics]
         dts = R.plane_dtypes(self.params)
-        outs = [[np.empty(s, dt) for s, dt in zip(shp[i], dts)] if i in sel else None for i in range(n)]
+        if into is not None:
+            if len(into) != n:
+                raise ValueError("into: one entry per picture")
+            for i in sel:
+                for k in range(3):
+                    a = into[i][k]
+                    if a.shape != tuple(shp[i][k]) or a.dtype != dts[k] or not a.flags.c_contiguous or not a.flags.writeable:
+                        raise ValueError("into: picture %d plane %d does not match the plane layout" % (i, k))
+            outs = [list(into[i]) if i in sel else None for i in range(n)]
+        else:
+            outs = [[np.empty(s, dt) for s, dt in zip(shp[i], dts)] if i in sel else None for i in range(n)]
         recs = ([[np.empty(s, dt) for s, dt in zip(shp[i], dts)] if i in sel else None for i in range(n)]
                 if with_recon else None)
         arr = (_lib.PictureC * n)()

@@ -651,3 +651,29 @@ def test_tile_halo_equals_whole_picture(recon_mod, w, h, ctb_log2, tiles_xy, per
         for c in range(3):
             s = 0 if c == 0 else 1
             np.testing.assert_array_equal(planes[c], ref[c][y0 >> s:y1 >> s, x0 >> s:x1 >> s], err_msg="tile %d c%d" % (t, c))
+
+
+def test_download_into_frame_pool(recon_mod):
+    """ctx.download(into=frames) refills a caller's frame pool (bench.py's PCIe leg): same planes as a
+    fresh download, the pool's arrays themselves are written, and a mismatched pool is refused."""
+    params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5)
+    a = [synth.make_picture(params, 7100 + s, perf=bool(s)) for s in range(2)]
+    b = [synth.make_picture(params, 7200 + s, perf=bool(s)) for s in range(2)]
+    with recon_mod.ReconContext(params) as ctx:
+        ba, bb = ctx.upload(a), ctx.upload(b)
+        ctx.run(ba)
+        ctx.run(bb)
+        pool = ctx.download(ba)
+        want_b = ctx.download(bb)
+        got = ctx.download(bb, into=pool)
+        assert all(got[i][k] is pool[i][k] for i in range(2) for k in range(3))
+        for i in range(2):
+            for k in range(3):
+                np.testing.assert_array_equal(pool[i][k], want_b[i][k])
+        bad = [[p.copy() for p in f] for f in pool]
+        bad[1][2] = bad[1][2][:, :-1].copy()
+        with pytest.raises(ValueError):
+            ctx.download(ba, into=bad)
+        with pytest.raises(ValueError):
+            ctx.download(ba, into=pool[:1])
+        ba.free(); bb.free()
