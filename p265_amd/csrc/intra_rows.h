@@ -216,6 +216,10 @@ using WaveLds = WaveLdsT<uint8_t>;
 #ifndef P265R_LATE_REC
 #define P265R_LATE_REC 0                 // 1: the next job's record read after the job (A/B: slower)
 #endif
+#ifndef P265R_QUAD_COMPOSED
+#define P265R_QUAD_COMPOSED 0            // A/B: composed quad-stage references in the cross-group kernel (quad_stage_c):
+                                         // parity green, C5 intra 2.11-2.14 -> 2.31-2.34 ms (3 reps): not kept
+#endif
 #ifndef P265R_TR_DEFER
 #define P265R_TR_DEFER 1                 // 0: wait for the top-right CTU before the CTU starts (A/B knob)
 #endif
@@ -869,6 +873,114 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
     }
 }
 
+// One quad stage with COMPOSED reference reads (the latency layouts, P265R_QUAD_COMPOSED): every reference
+// the stage's prediction reads is taken straight from its source register -- Clip3(fa, la, i) mapped by the
+// stage's affine map onto the external samples or the stages already reconstructed -- instead of first
+// gathering the stage's reference vector and then reading it: one ds_bpermute round trip per stage instead
+// of two, for a few more VALU (the index map per read) and the stage's AngTab4 entry read ahead with the
+// external gather.  Luma stages with two sources read one packed register (rec | ext << 16); chroma values
+// are Cb | Cr pairs already, so a chroma read takes both candidates and selects.  Same arithmetic as
+// quad_stage (fast_pred<2, false, true> / cpred<2, true>), bit for bit.
+template <int Q, bool CH, typename T = uint8_t>
+__device__ __forceinline__ int quad_stage_c(int rec, int ext, int lane, int mode, bool none, int fa, int la,
+                                            uint32_t te, int r16, int qid, int x, int y, int maxv = 255) {
+    constexpr int n = 4;
+    const int half_v = (maxv + 1) >> 1;
+    const uint32_t none_v = CH ? (uint32_t)half_v * 0x00010001u : (uint32_t)half_v;
+    // source of substituted reference s: (lane of the source register, from ext?)
+    auto src_lane = [](int s) -> int {
+        if constexpr (Q == 0) return s <= 8 ? 8 - s : s + 4;
+        else if constexpr (Q == 1) return s < 8 ? 59 - 8 * s : s + 8;
+        else if constexpr (Q == 2) return s <= 8 ? 12 - s : s + 15;
+        else return s <= 8 ? 91 - 8 * s : s + 19;
+    };
+    auto from_ext = [](int s) -> bool {
+        if constexpr (Q == 0) return true;
+        else if constexpr (Q == 1) return s >= 8;
+        else if constexpr (Q == 2) return s <= 8;
+        else return false;
+    };
+    // luma, two sources: one packed register, the half picked after the read
+    const int P = (Q == 1 || Q == 2) && !CH ? (int)(((uint32_t)rec & 0xffffu) | (uint32_t)ext << 16) : (Q == 0 ? ext : rec);
+    auto cref = [&](int i) -> uint32_t {                           // per-lane reference index i
+        const int s = min(max(i, fa), la);
+        const int sl = src_lane(s) << 2;
+        uint32_t v;
+        if constexpr (Q == 0 || Q == 3) {
+            v = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, P);
+        } else if constexpr (!CH) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, P);
+            v = from_ext(s) ? w >> 16 : w & 0xffffu;
+        } else {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, rec), b = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, ext);
+            v = from_ext(s) ? b : a;
+        }
+        if constexpr (Q == 0) v = none ? none_v : v;
+        return v;
+    };
+    auto uref = [&](int i) -> uint32_t {                           // wave-uniform reference index i
+        const int s = __builtin_amdgcn_readfirstlane(min(max(i, fa), la));
+        const int sl = src_lane(s);
+        uint32_t v;
+        if constexpr (Q == 0 || Q == 3) {
+            v = (uint32_t)__builtin_amdgcn_readlane(P, sl);
+        } else if constexpr (!CH) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(P, sl);
+            v = from_ext(s) ? w >> 16 : w & 0xffffu;
+        } else {
+            v = from_ext(s) ? (uint32_t)__builtin_amdgcn_readlane(ext, sl) : (uint32_t)__builtin_amdgcn_readlane(rec, sl);
+        }
+        if constexpr (Q == 0) v = none ? none_v : v;
+        return v;
+    };
+    const bool in = (lane >= n && lane < 2 * n) || (lane > 2 * n && lane <= 3 * n);   // DC sum lanes
+    if constexpr (CH) {
+        constexpr uint32_t rnd = (uint32_t)n * 0x00010001u, msk = (0xffffu >> 3) * 0x00010001u;
+        uint32_t pred;
+        if (mode >= 2) {                                           // AngTab4 entry (modes 10 / 26 included: fact 0)
+            const uint32_t a = cref((int)((te & 0xffu) >> 2)), b = cref((int)(((te >> 8) & 0xffu) >> 2));
+            pred = ((pmul<T>(te >> 24, a) + pmul<T>((te >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+        } else if (mode == 0) {
+            const uint32_t lft = cref(2 * n - 1 - y), top = cref(2 * n + 1 + x);
+            const uint32_t sum = pmul<T>(n - 1 - x, lft) + pmul<T>(x + 1, uref(3 * n + 1)) + pmul<T>(n - 1 - y, top) +
+                                 pmul<T>(y + 1, uref(n - 1)) + rnd;
+            pred = (sum >> 3) & msk;
+        } else {
+            const uint32_t vk = cref(lane);
+            const uint32_t sum = (uint32_t)wave_sum<false, 1>(in ? (int)vk : 0, 0) + rnd;
+            pred = (sum >> 3) & msk;
+        }
+        const int rq = (int)cquad_recon(pred, (uint32_t)r16, maxv);
+        return qid == Q ? rq : rec;
+    } else {
+        int pred;
+        if (mode >= 2) {
+            if (P265R_HV_FAST && (mode & ~16) == 10) {             // modes 10 / 26: copies + boundary smoothing
+                const bool vert = mode >= 18;
+                pred = (int)cref(vert ? 2 * n + 1 + x : 2 * n - 1 - y);
+                const int b = (int)cref(vert ? 2 * n - 1 - y : 2 * n + 1 + x);
+                const int edge = clip_pel((int)uref(vert ? 2 * n + 1 : 2 * n - 1) + ((b - (int)uref(2 * n)) >> 1), maxv);
+                pred = (vert ? x : y) == 0 ? edge : pred;
+            } else {
+                const int a = (int)cref((int)((te & 0xffu) >> 2)), b = (int)cref((int)(((te >> 8) & 0xffu) >> 2));
+                pred = (__mul24((int)(te >> 24), a) + __mul24((int)((te >> 16) & 0xffu), b) + 16) >> 5;
+            }
+        } else if (mode == 0) {
+            const int lft = (int)cref(2 * n - 1 - y), top = (int)cref(2 * n + 1 + x);
+            pred = (__mul24(n - 1 - x, lft) + __mul24(x + 1, (int)uref(3 * n + 1)) + __mul24(n - 1 - y, top) +
+                    __mul24(y + 1, (int)uref(n - 1)) + n) >> 3;
+        } else {
+            const int vk = (int)cref(lane);
+            const int lft = (int)cref(2 * n - 1 - y), top = (int)cref(2 * n + 1 + x);
+            const int dc = (wave_sum<false, 1>(in ? vk : 0, 0) + n) >> 3;
+            const int sl = x == 0 ? lft : dc, st = y == 0 ? top : dc;
+            pred = (x == 0 || y == 0) ? (sl + st + 2 * dc + 2) >> 2 : dc;
+        }
+        const int rq = clip_pel(pred + r16, maxv);
+        return qid == Q ? rq : rec;
+    }
+}
+
 // 4x4 QUAD job (J5_QUAD, intra_prep.h): the four fast 4x4 TBs of one 8x8 luma region (CH =
 // false), or the four Cb+Cr 4x4 pairs of one 8x8 chroma region (CH = true), in one job.  Lane
 // l = region sample (l & 7, l >> 3); the 25 external reference samples (column x = -1, rows
@@ -877,7 +989,7 @@ __device__ __forceinline__ int quad_stage(int rec, int ext, int lane, int mode, 
 // buffer, and pack them), the four stages pass their samples to each other through registers
 // (ds_bpermute), and the region is written to LDS once.  r16 = this lane's residual sample
 // (chroma: the packed Cb | Cr << 16 pair); line_top = the row above the CTU (chroma: the Cb line).
-template <bool CH, typename T = uint8_t>
+template <bool CH, typename T = uint8_t, bool COMP = false>
 __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, uint32_t cw, uint32_t w0, uint32_t w1,
                                            uint32_t w2, uint32_t tab, int r16, int lane, int maxv = 255) {
     constexpr int ist = CH ? 32 : 64, last = ist - 1;           // interior stride, last row / column
@@ -907,6 +1019,19 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
     // (pinned at the stage start: the read then shares the gather's LDS wait instead of adding one)
     auto ang = [&](uint32_t m) { uint32_t te = *lds32(tab + m * 64u + pos4); asm volatile("" : "+v"(te)); return te; };
     int rec = 0;
+    if constexpr (COMP) {
+        // composed stages: the four AngTab4 entries read with the external gather (one LDS round trip)
+        const uint32_t m0 = (w0 >> 17) & 63u, m1 = (w0 >> 23) & 63u, m2 = w1 & 63u, m3 = (w1 >> 6) & 63u;
+        const uint32_t t0 = ang(m0), t1 = ang(m1), t2 = ang(m2), t3 = ang(m3);
+        rec = quad_stage_c<0, CH, T>(rec, ext, lane, (int)m0, (w0 >> 29) & 1u, (int)((w1 >> 14) & 31u), (int)((w1 >> 19) & 31u),
+                                     t0, r16, qid, xs, ys, maxv);
+        rec = quad_stage_c<1, CH, T>(rec, ext, lane, (int)m1, false, (int)((w1 >> 24) & 31u), (int)(w2 & 31u),
+                                     t1, r16, qid, xs, ys, maxv);
+        rec = quad_stage_c<2, CH, T>(rec, ext, lane, (int)m2, false, (int)((w2 >> 5) & 31u), (int)((w2 >> 10) & 31u),
+                                     t2, r16, qid, xs, ys, maxv);
+        rec = quad_stage_c<3, CH, T>(rec, ext, lane, (int)m3, false, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
+                                     t3, r16, qid, xs, ys, maxv);
+    } else {
     P265R_MARK("quad_stage0");
     {
         const uint32_t m = (w0 >> 17) & 63u;
@@ -930,6 +1055,7 @@ __device__ __forceinline__ void recon_quad(uint32_t lbase, uint32_t line_top, ui
         const uint32_t m = (w1 >> 6) & 63u;
         rec = quad_stage<3, CH, T>(rec, ext, lane, (int)m, (w1 >> 13) & 1u, (int)((w2 >> 15) & 31u), (int)((w2 >> 20) & 31u),
                                    ang(m), r16, qid, xs, ys, maxv);
+    }
     }
     P265R_MARK("quad_store");
     const uint32_t da = lbase + (CH ? kOrgCT<T> : kOrgLT<T>) + (uint32_t)ofs + (uint32_t)((lane >> 3) * ist + (lane & 7));
@@ -1422,8 +1548,10 @@ void intra_rows_kernel(const DevPic* __restrict__ pics,
                 // (8 bits: the constant 255 folds into every job function, as before the 16-bit path)
                 const int mv = PB == 1 ? 255 : maxv;
                 if (w5 & J5_QUAD) {
-                    if ((w0 >> 15) & 3u) recon_quad<true, T>(lbase, tcb, cr_off, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, mv);
-                    else recon_quad<false, T>(lbase, tl, 0u, w0, w1, w2, tab, c16, ln, mv);
+                    // (the latency layout reads the quad stages' references composed: one round trip per stage)
+                    constexpr bool kComp = XG && P265R_QUAD_COMPOSED;
+                    if ((w0 >> 15) & 3u) recon_quad<true, T, kComp>(lbase, tcb, cr_off, w0, w1, w2, tab, (int)((uint32_t)c16 | (uint32_t)c16m << 16), ln, mv);
+                    else recon_quad<false, T, kComp>(lbase, tl, 0u, w0, w1, w2, tab, c16, ln, mv);
                 } else if (w5 & J5_FAST) {
                     switch (sel) {
                         case 0: recon_fast<2, false, T>(lbase, tl, w0, w1, w5, c16, ln, tab, mv); break;
