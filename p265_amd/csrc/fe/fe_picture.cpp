@@ -693,8 +693,11 @@ private:
         int n = 1 << log2;
         uint32_t off;
         int16_t* blk = coef_alloc((size_t)n * n, off);
+        // the engine lives in registers for the whole TB (copied back at the end)
+        Cabac e = cabac_;
+        uint16_t* const cx = ctx_;
         int tskip = 0;
-        if (pps_.transform_skip && !cu_bypass_ && log2 <= 2) tskip = dec(C_TSKIP + (c ? 1 : 0));
+        if (pps_.transform_skip && !cu_bypass_ && log2 <= 2) tskip = e.decision(cx[C_TSKIP + (c ? 1 : 0)]);
         *tskip_out = tskip;
         // last_sig_coeff_x/y_prefix (TR, cMax (log2 << 1) - 1), suffix (FL bypass)
         int off_ctx, shift;
@@ -702,16 +705,16 @@ private:
         else { off_ctx = 15; shift = log2 - 2; }
         int cmax = (log2 << 1) - 1;
         int px = 0, py = 0;
-        while (px < cmax && dec(C_LAST_X + off_ctx + (px >> shift))) ++px;
-        while (py < cmax && dec(C_LAST_Y + off_ctx + (py >> shift))) ++py;
+        while (px < cmax && e.decision(cx[C_LAST_X + off_ctx + (px >> shift)])) ++px;
+        while (py < cmax && e.decision(cx[C_LAST_Y + off_ctx + (py >> shift)])) ++py;
         int last_x = px, last_y = py;
         if (px > 3) {
             int nb = (px >> 1) - 1;
-            last_x = (1 << nb) * (2 + (px & 1)) + (int)cabac_.bypass_bits(nb);
+            last_x = (1 << nb) * (2 + (px & 1)) + (int)e.bypass_bits(nb);
         }
         if (py > 3) {
             int nb = (py >> 1) - 1;
-            last_y = (1 << nb) * (2 + (py & 1)) + (int)cabac_.bypass_bits(nb);
+            last_y = (1 << nb) * (2 + (py & 1)) + (int)e.bypass_bits(nb);
         }
         // scanIdx (7.4.9.11): mode dependent for 4x4, and 8x8 luma
         int scan = 0;
@@ -733,9 +736,6 @@ private:
         const bool sdh = pps_.sign_data_hiding && !cu_bypass_;
         int greater1_state = 1;   // "c1" carried across sub-blocks (9.3.4.2.6)
         bool first_sb_done = false;
-        // the engine lives in registers for the whole TB (copied back at the end)
-        Cabac e = cabac_;
-        uint16_t* const cx = ctx_;
         // sig_coeff_flag contexts per position of a sub-block (9.3.4.2.5), tabulated (kSigCtx)
         const int cc = c ? 1 : 0;
         for (int i = last_sb; i >= 0; --i) {
