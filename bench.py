@@ -184,7 +184,7 @@ def parse(argv=None):
                     help="N > 1: comma-separated HIP device of each local rank (default: local rank i on device i); "
                          "ranks sharing a device need --no-rccl (tests: --gpus 2 --device-map 0,0 --no-rccl)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive back-end leg")
-    ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 9, 10),
+    ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 9, 10, 11, 12),
                     help="c3: BitDepth of the synthetic pictures (9 / 10: the Main 10 path -- uint16 planes, per-diagonal "
                          "intra kernel, loopfilter16.h; not the headline)")
     return ap.parse_args(argv)
@@ -545,7 +545,7 @@ def build_workload(a, rank, world):
         pics = [uniq[i % a.unique] for i in range(a.frames)]
         cfg = {"workload": "C3/C4: 1080p all-intra + %sSAO, %d pictures per GPU per step (%d distinct)%s"
                            % ("deblocking + " if a.deblocking else "", a.frames, a.unique,
-                              "" if a.bit_depth == 8 else ", BitDepth %d (Main 10 path, not the headline)" % a.bit_depth),
+                              "" if a.bit_depth == 8 else ", BitDepth %d (16-bit path, not the headline)" % a.bit_depth),
                "bit_depth": a.bit_depth,
                "pictures_per_gpu": a.frames, "ctus_per_picture": len(pics[0].ctus), "ctb": 64,
                "parallelism": "picture-sharded x%d (picture f -> rank f mod N)" % world}
@@ -852,7 +852,8 @@ def main(argv=None):
         "data": "synthetic: seeded all-intra records with sanity.bin statistics (p265_amd/synth.py)",
         "config": cfg,
         "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel" if a.bit_depth == 8 else
-                     "intra_rows_kernel<..., uint16_t>", "achieved": round(achieved, 2),
+                     ("intra_rows_kernel<..., uint16_t>" if a.bit_depth <= 10 else
+                      "intra_step_kernel<uint16_t> (one launch per anti-diagonal)"), "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
                                         % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
@@ -864,7 +865,9 @@ def main(argv=None):
                               "HBM (DESIGN.md §4); see issue_rates" if a.bit_depth == 8 else
                               "achieved / avg_launch_ms: the 16-bit row pipeline (one workgroup per CU: twice the "
                               "LDS per wave), the batch alone (W = 12); the Main 10 path, not the headline "
-                              "(DESIGN.md §4)")},
+                              "(DESIGN.md §4)" if a.bit_depth <= 10 else
+                              "achieved / avg_launch_ms of one anti-diagonal launch (BitDepth 11-12: the per-diagonal "
+                              "kernel, one workgroup per CTU of the diagonal); not the headline (DESIGN.md §4)")},
         "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms) if a.bit_depth == 8 else None,
         "intra_jobs_per_launch": {"luma": jl, "chroma": jch},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
@@ -878,7 +881,8 @@ def main(argv=None):
     if w8:
         builds["w8_alone"] = {"avg_launch_ms": round(w8, 4),
                               "frac": round(bytes_per_launch / (w8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    out["roofline"]["builds"] = builds
+    if a.bit_depth <= 10:
+        out["roofline"]["builds"] = builds
     if a.workload == "c5":
         out["unit_latency_ms"] = c5_unit_latency(ctxs[0][0], cpu_sample, a.steps)
         if a.c5_world:

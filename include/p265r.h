@@ -73,7 +73,7 @@ typedef struct p265r_params {
     uint16_t pic_width;               /* pic_width_in_luma_samples                */
     uint16_t pic_height;              /* pic_height_in_luma_samples               */
     uint8_t  chroma_format_idc;       /* 1 (4:2:0) only                           */
-    uint8_t  bit_depth_luma;          /* BitDepthY: 8, or 9..10 (Main 10: uint16_t planes) */
+    uint8_t  bit_depth_luma;          /* BitDepthY: 8, or 9..12 (uint16_t planes)   */
     uint8_t  bit_depth_chroma;        /* BitDepthC: equal to bit_depth_luma        */
     uint8_t  ctb_log2_size;           /* CtbLog2SizeY, 4..6                       */
     uint8_t  min_tb_log2_size;        /* MinTbLog2SizeY, 2..5                     */
@@ -131,7 +131,7 @@ typedef struct p265r_picture {
                                  (pcm_loop_filter_disabled && pcm, or cu_transquant_bypass)   */
     void*            out[3];  /* decoded (post-deblocking, post-SAO) planes Y, Cb, Cr; stride =
                                  plane width in samples; uint8_t samples at BitDepth 8, uint16_t
-                                 at 9..10.  NULL = do not download                              */
+                                 at 9..12.  NULL = do not download                              */
     void*            recon[3];/* optional in-loop-filter input (reconstruction before deblocking
                                  and SAO), same layout; NULL = skip.  Written by download, or
                                  read by upload with P265R_PIC_RECON_INPUT                     */

@@ -15,8 +15,9 @@
 // write; no intermediate deblocked plane exists.
 //
 // Edge information comes from dbk_map_kernel: one byte per 8x8 luma block,
-//   bits 0..5 Qp'Y of its CU (= QpY at 8 bits; loopfilter16.h subtracts QpBdOffsetY), bit 6 its left side is a transform-block edge,
-//   bit 7 its top side is a transform-block edge.
+//   bits 0..5 Qp'Y of its CU (= QpY at 8 bits), bit 6 its left side is a transform-block edge,
+//   bit 7 its top side is a transform-block edge.  Above 8 bits one uint16 per block: bits 0..7
+//   Qp'Y (loopfilter16.h subtracts QpBdOffsetY), bit 8 left edge, bit 9 top edge.
 // In 4:2:0 intra pictures every TB boundary on the 8x8 grid is an edge with bS = 2
 // (8.7.2.4: intra on either side); prediction-block edges of NxN CUs sit at 4-sample
 // offsets and never reach the grid.  Every 8x8 block is written by exactly one luma TB:
@@ -32,6 +33,9 @@
 namespace p265r {
 
 enum : uint8_t { DBK_V = 0x40, DBK_H = 0x80, DBK_QP = 0x3f };
+// BitDepth > 8 (loopfilter16.h): Qp'Y reaches 51 + 6 * (BitDepth - 8) = 75 at 12 bits, past 6 bits, so the
+// map holds uint16 entries there: Qp'Y in the low byte, the edge bits above it.
+enum : uint16_t { DBK16_V = 0x100, DBK16_H = 0x200, DBK16_QP = 0xff };
 
 // Table 8-12 tC' (Q = 0..53); beta' has the closed form used in dbk_beta()
 __constant__ uint8_t c_tc_table[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
@@ -52,7 +56,9 @@ __device__ __forceinline__ int nib4(int v) { return (v ^ 8) - 8; }   // 4-bit tw
 // ---------------------------------------------------------------------------------------
 // Edge map: grid (CTUs, pictures), one wave per CTU walks its TBs.
 // ---------------------------------------------------------------------------------------
+template <typename M>        // uint8_t: BitDepth 8 (DBK_*); uint16_t: BitDepth 9..12 (DBK16_*)
 __global__ __launch_bounds__(64) void dbk_map_kernel(const DevPic* __restrict__ pics, Geo g) {
+    constexpr int EV = sizeof(M) == 1 ? DBK_V : DBK16_V, EH = sizeof(M) == 1 ? DBK_H : DBK16_H;
     const DevPic* P = pics + blockIdx.y;
     if (P265R_RAGGED && g.ragged) {                                              // grid: the context's CTU count
         g = pic_geo(g, (uint32_t)__builtin_amdgcn_readfirstlane((int)P->wh));
@@ -60,20 +66,20 @@ __global__ __launch_bounds__(64) void dbk_map_kernel(const DevPic* __restrict__ 
     }
     const p265r_ctu me = P->ctus[blockIdx.x];
     const p265r_tb* tbs = P->tbs + me.tb_begin;
-    uint8_t* map = P->dbk_map;
+    M* map = reinterpret_cast<M*>(P->dbk_map);
     for (int t = threadIdx.x; t < me.tb_count; t += 64) {
         const p265r_tb tb = tbs[t];
         if (tb.c_idx != 0) continue;
-        const int qpy = (int)tb.qp;                  // Qp'Y (0..63 up to BitDepth 10)
+        const int qpy = (int)tb.qp;                  // Qp'Y (0..63 up to BitDepth 10, 0..75 at 12)
         const int bx0 = tb.x >> 3, by0 = tb.y >> 3;
         if (tb.log2_size == 2) {
-            if ((tb.x & 7) == 0 && (tb.y & 7) == 0) map[by0 * g.nf_w + bx0] = (uint8_t)(qpy | DBK_V | DBK_H);
+            if ((tb.x & 7) == 0 && (tb.y & 7) == 0) map[by0 * g.nf_w + bx0] = (M)(qpy | EV | EH);
             continue;
         }
         const int n8 = 1 << (tb.log2_size - 3);
         for (int j = 0; j < n8; ++j)
             for (int i = 0; i < n8; ++i)
-                map[(by0 + j) * g.nf_w + bx0 + i] = (uint8_t)(qpy | (i == 0 ? DBK_V : 0) | (j == 0 ? DBK_H : 0));
+                map[(by0 + j) * g.nf_w + bx0 + i] = (M)(qpy | (i == 0 ? EV : 0) | (j == 0 ? EH : 0));
     }
 }
 

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void loopfilter16_kernel(const DevPic* __restr
     constexpr int T = 256;
     __shared__ uint16_t s_l[RL * RL];
     __shared__ uint16_t s_c[2][RC * RC];
-    __shared__ uint8_t s_map[NB * NB];
+    __shared__ uint16_t s_map[NB * NB];
     __shared__ uint8_t s_nf[NB * NB];
     __shared__ LfCtu s_ctu[9];
     __shared__ uint32_t s_allow;
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void loopfilter16_kernel(const DevPic* __restr
         const int bx = (x0 >> 3) - 1 + i % NB, by = (y0 >> 3) - 1 + i / NB;
         const bool in = bx >= 0 && by >= 0 && bx < g.nf_w && by < nf_h;
         const size_t o = (size_t)by * g.nf_w + bx;
-        if (DBK) s_map[i] = in ? P->dbk_map[o] : 0;
+        if (DBK) s_map[i] = in ? reinterpret_cast<const uint16_t*>(P->dbk_map)[o] : 0;
         s_nf[i] = in && P->nofilter ? P->nofilter[o] : 0;
     }
     {
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void loopfilter16_kernel(const DevPic* __restr
         };
         constexpr int N_DBK = NLE * WL + 2 * NCE * WC;
         for (int dir = 0; dir < 2; ++dir) {                  // 0: vertical edges, 1: horizontal edges
-            const uint8_t ebit = dir ? DBK_H : DBK_V;
+            const int ebit = dir ? DBK16_H : DBK16_V;
             for (int t = tid; t < N_DBK; t += T) {
                 if (t < NLE * WL) {
                     const int i = t / WL, j = t % WL;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void loopfilter16_kernel(const DevPic* __restr
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
                         for (int k = 0; k < 4; ++k) { Pm[a][k] = at(a, k, false); Qm[a][k] = at(a, k, true); }
-                    dbk_luma_seg16(Pm, Qm, (s_map[bp] & DBK_QP) - qp_off, (mq & DBK_QP) - qp_off, nib4(offs & 15),
+                    dbk_luma_seg16(Pm, Qm, (s_map[bp] & DBK16_QP) - qp_off, (mq & DBK16_QP) - qp_off, nib4(offs & 15),
                                    nib4(offs >> 4), s_nf[bp] != 0, s_nf[bq] != 0, g.bd[0]);
 #pragma unroll
                     for (int a = 0; a < 3; ++a)
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void loopfilter16_kernel(const DevPic* __restr
                     if (!(mq & ebit)) continue;
                     const int offs = edge_offs(xp, yp, xq, yq);
                     if (offs < 0) continue;
-                    const int qpi = ((((mq & DBK_QP) - qp_off) + ((s_map[bp] & DBK_QP) - qp_off) + 1) >> 1) +
+                    const int qpi = ((((mq & DBK16_QP) - qp_off) + ((s_map[bp] & DBK16_QP) - qp_off) + 1) >> 1) +
                                     (c ? g.cqp[1] : g.cqp[0]);
                     const int tc = (int)c_tc_table[min(max(qpc_table(qpi) + 2 + 2 * nib4(offs >> 4), 0), 53)] << (g.bd[1] - 8);
                     const int maxc = (1 << g.bd[1]) - 1;

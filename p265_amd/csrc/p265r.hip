@@ -518,9 +518,9 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
     *out = nullptr;
     const p265r_params& p = *params;
     if (!params_ok(p)) return P265R_EINVAL;
-    // BitDepth 8 (uint8_t planes, the row pipeline) or 9..10 with one depth for luma and chroma (Main 10:
-    // uint16_t planes, the per-diagonal intra kernel and loopfilter16.h)
-    if (p.bit_depth_luma < 8 || p.bit_depth_luma > 10 || p.bit_depth_chroma != p.bit_depth_luma || p.scaling_list_enabled > 1)
+    // BitDepth 8 (uint8_t planes) or 9..12 with one depth for luma and chroma (uint16_t planes; 13..14 would
+    // need SaoOffsetVal beyond the int8 of the CTU record)
+    if (p.bit_depth_luma < 8 || p.bit_depth_luma > 12 || p.bit_depth_chroma != p.bit_depth_luma || p.scaling_list_enabled > 1)
         return P265R_EUNSUPPORTED;
     const int n = p265r_device_count();
     if (n < 0) return n;
@@ -557,8 +557,9 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     // 16-bit samples: the row pipeline while a W = 8 workgroup's LDS tiles and two line-buffer slots fit
-    // 160 KB (pictures up to ≈ 4K wide), else the per-diagonal kernel
-    if (g.pel16 && rows_lds_bytes<uint16_t>(g, 8, 2) > 160 * 1024) ctx->schedule = 0;
+    // 160 KB (pictures up to ≈ 4K wide), else the per-diagonal kernel; BitDepth 11..12 always the latter
+    // (the row pipeline's packed Cb | Cr arithmetic needs every weighted chroma sum below 2^16)
+    if (g.pel16 && (p.bit_depth_luma > 10 || rows_lds_bytes<uint16_t>(g, 8, 2) > 160 * 1024)) ctx->schedule = 0;
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';
@@ -756,7 +757,8 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
     size_t n_nf = 0;
     for (int i = 0; i < n_pics; ++i) n_nf += pics[i].nofilter ? 1 : 0;
     off = align_up(off + nf_bytes * n_nf, 256);
-    const size_t o_map = off; if (dbk) off = align_up(off + nf_bytes * n_pics, 256);
+    const size_t map_bytes = nf_bytes << g.pel16;                  // uint16 entries above 8 bits (loopfilter.h)
+    const size_t o_map = off; if (dbk) off = align_up(off + map_bytes * n_pics, 256);
     const size_t o_rec = off; off += pic_plane_bytes * n_pics;
     const size_t o_out = off; if (lf) off += pic_plane_bytes * n_pics;
     const size_t total = align_up(off, 256);
@@ -884,7 +886,7 @@ int p265r_batch_upload(p265r_ctx* ctx, const p265r_picture* pics, int n_pics, p2
         dp.rec[0] = rec;
         dp.rec[1] = rec + align_up(plane_bytes[0], 256);
         dp.rec[2] = dp.rec[1] + align_up(plane_bytes[1], 256);
-        dp.dbk_map = dbk ? dbase + o_map + nf_bytes * i : nullptr;
+        dp.dbk_map = dbk ? dbase + o_map + map_bytes * i : nullptr;
         dp.pool_rel = -(int32_t)((o_res - o_pool) / sizeof(int16_t));
         dp.zero_off = (uint32_t)pool_total;
         dp.wh = (uint32_t)psize[i][0] | (uint32_t)psize[i][1] << 16;
@@ -1128,7 +1130,8 @@ int p265r_batch_run(p265r_ctx* ctx, p265r_batch* b) {
     }
     if (b->dbk) {
         // deblocking edge / QpY map: depends on the records only
-        dbk_map_kernel<<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);   // (context-size grid)
+        if (g.pel16) dbk_map_kernel<uint16_t><<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);
+        else dbk_map_kernel<uint8_t><<<dim3(ctx->n_ctus, b->n_pics), 64, 0, s>>>(b->d_pics, g);   // (context-size grid)
         ++tm.residual_launches;
     }
     HIP_TRY(hipGetLastError());

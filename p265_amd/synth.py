@@ -99,7 +99,8 @@ def make_picture(params, seed, perf=True, tiles=(1, 1), n_slices=1, sao=True, ts
 
     def qps():
         # QpY, then qP' of each component (+ QpBdOffset): what the TB records carry
-        qy = 32 if perf else int(rng.integers(22 - offy, 38))
+        # (above 10 bits up to QpY 51: Qp'Y then passes 63, the deblocking map's 8-bit limit)
+        qy = 32 if perf else int(rng.integers(22 - offy, 52 if bdy > 10 else 38))
         qcb, qcr = frontend.chroma_qp(qy, 0, 0, offc)
         return qy + offy, qcb + offc, qcr + offc
 

@@ -23,7 +23,7 @@ oracle/recon_oracle.py equal the reference's (transform.py:5-72, intra.py:15-22)
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python3 -B tests/golden/gen_component_fixture.py [--bit-depth 10]
 
---bit-depth 10 (Main 10) writes ref_components_bd10.npz / .json: the same functions with the SPS's
+--bit-depth 10 (Main 10) and 12 write ref_components_bd10.npz / bd12.npz (+ .json): the same functions with the SPS's
 BitDepthY = BitDepthC = 10 and QpBdOffset = 12 (scaling.py:14-26 bdShift and qP, reconstruction.py:25
 and utils.py:11-15 clip, intra.py:241 substitution default, intra.py:280-281 strong-filter threshold,
 intra.py:160 edge-filter clip), samples 0..1023 and QpY -12..51.  The 8-bit run is unchanged.
@@ -270,7 +270,7 @@ def main_scaling():
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 10))
+    ap.add_argument("--bit-depth", type=int, default=8, choices=(8, 10, 12))
     ap.add_argument("--scaling", action="store_true", help="the ScalingFactor vectors (ref_scaling.npz) instead")
     args = ap.parse_args()
     if args.scaling:

@@ -60,7 +60,7 @@ def test_invalid_params_rejected_before_device():
     assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EINVAL      # version 0
     p.version, p.pic_width, p.pic_height, p.chroma_format_idc = 2, 64, 64, 1
     p.ctb_log2_size, p.min_tb_log2_size, p.max_tb_log2_size = 6, 2, 5
-    for bl, bc in ((12, 12), (10, 8), (8, 9), (7, 7)):        # Main 10: one depth of 8..10 for luma and chroma
+    for bl, bc in ((13, 13), (10, 8), (8, 9), (7, 7)):        # one depth of 8..12 for luma and chroma
         p.bit_depth_luma, p.bit_depth_chroma = bl, bc
         assert lib.p265r_create(0, ctypes.byref(p), ctypes.byref(h)) == _lib.EUNSUPPORTED
     assert lib.p265r_wait(None) == _lib.EINVAL

@@ -44,6 +44,8 @@ CASES = {
     "main10_tiles_wpp_bypass": dict(bit_depth=10, tiles=(2, 2), wpp=True, bypass=True, qp_delta_depth=0),
     "main9_chroma_offsets": dict(bit_depth=9, slice_chroma_offsets=(3, -5), cb_qp_offset=-4, cr_qp_offset=6,
                                  qp_delta_depth=1, deblocking="override", slices=[(0, False), (20, False)]),
+    # BitDepth 12 (QpBdOffset 24, SaoOffsetVal << 2, PCM at 11 / 10 bits)
+    "main12_tiles": dict(bit_depth=12, tiles=(2, 2), qp_delta_depth=1, init_qp=4, slice_qp_delta=-25, pcm=(3, 4, True)),
     # scaling lists (7.3.4): enabled with the default lists, random lists in the SPS, SPS lists overridden by the PPS
     "scaling_default": dict(scaling_lists="default"),
     "scaling_sps": dict(scaling_lists="sps", tskip=True),

@@ -58,3 +58,16 @@ def test_synthetic_main10(ctb_log2, w, h, tiles, slices):
     _same(params, pics)
     got = c_oracle.decode(params, pics[:1])[0][1]
     assert got[0].dtype == np.uint16 and got[0].max() > 255
+
+
+@pytest.mark.parametrize("bd", [11, 12])
+def test_synthetic_high_bit_depth(bd):
+    """BitDepth 11 / 12 (uint16 planes; QpBdOffset 18 / 24, SAO offsets << (BitDepth - 10)): the C twin equals
+    the Python oracle with deblocking, PCM, bypass, transform skip, tiles and slices."""
+    params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5, bit_depth_luma=bd, bit_depth_chroma=bd,
+                           pps_cb_qp_offset=1, pps_cr_qp_offset=-2)
+    pics = [synth.make_picture(params, 1900 + bd + s, perf=bool(s), tiles=(2, 2), n_slices=2, lf_across_slices=None,
+                               tskip_rate=0.3, bypass_rate=0.05, pcm_rate=0.03, deblocking="random") for s in range(2)]
+    _same(params, pics)
+    got = c_oracle.decode(params, pics[:1])[0][1]
+    assert got[0].dtype == np.uint16 and got[0].max() > (1 << (bd - 1))

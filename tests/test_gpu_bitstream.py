@@ -57,6 +57,8 @@ CASES = {
     "main10": dict(bit_depth=10, pcm=(3, 4, True), bypass=True, qp_delta_depth=1, init_qp=14, slice_qp_delta=-18,
                    deblocking="override", slices=[(0, False), (20, False)]),
     "main10_tiles_wpp_ctb32": dict(bit_depth=10, tiles=(2, 2), wpp=True, ctb_log2=5, width=192, height=128),
+    "bd12_slices_pcm": dict(bit_depth=12, pcm=(3, 4, True), bypass=True, qp_delta_depth=1, init_qp=4,
+                            slice_qp_delta=-20, deblocking="override", slices=[(0, False), (20, False)]),
     # scaling lists: the front-end's ScalingFactor table (SPS lists, PPS override, defaults) into the residual kernels
     "scaling_sps_tskip": dict(scaling_lists="sps", tskip=True, qp_delta_depth=1),
     "scaling_pps_main10": dict(scaling_lists="pps", bit_depth=10, ctb_log2=5, width=160, height=96, frames=2),

@@ -137,9 +137,37 @@ def test_main10_row_pipeline_and_schedules(recon_mod, monkeypatch):
             np.testing.assert_array_equal(outs[i][c], ref[i][c], err_msg="steps pic %d c%d" % (i, c))
 
 
+@pytest.mark.parametrize("bd", [11, 12])
+@pytest.mark.parametrize("case", ["uniform", "tiles", "sao_only", "ragged"])
+def test_high_bit_depth_per_diagonal(recon_mod, bd, case):
+    """BitDepth 11 / 12 (the per-diagonal kernel intra_step_kernel<uint16_t>, loopfilter16.h / sao16.h, the
+    residual kernels at bdShift BitDepth + log2 - 5 / 20 - BitDepth) against the oracles."""
+    if case == "ragged":
+        big = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, bit_depth_luma=bd, bit_depth_chroma=bd)
+        pics = []
+        for k, (w, h) in enumerate([(264, 200), (128, 72), (40, 200)]):
+            pp = R.pic_params(big, R.Picture(ctus=None, tbs=None, coef=None, size=(w, h)))
+            pic = synth.make_picture(pp, 5800 + bd + k, perf=bool(k % 2), deblocking=bool(k % 2))
+            pic.size = (w, h)
+            pics.append(pic)
+        with recon_mod.ReconContext(big) as ctx:
+            assert ctx.describe()["schedule"] == "steps"
+        _check(recon_mod, big, pics, "bd%d ragged" % bd)
+        return
+    params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5 if case != "uniform" else 6,
+                           bit_depth_luma=bd, bit_depth_chroma=bd, loop_filter_across_tiles=0,
+                           pps_cb_qp_offset=-1, pps_cr_qp_offset=2)
+    kw = dict(uniform=dict(perf=False, deblocking=True),
+              tiles=dict(perf=False, tiles=(2, 2), n_slices=3, lf_across_slices=None, deblocking="random",
+                         bypass_rate=0.05, pcm_rate=0.03, tskip_rate=0.3),
+              sao_only=dict(perf=True, deblocking=False, tskip_rate=0.2, pcm_rate=0.02))[case]
+    pics = [synth.make_picture(params, 5900 + bd + s, **kw) for s in range(2)]
+    _check(recon_mod, params, pics, "bd%d %s" % (bd, case))
+
+
 def test_unsupported_bit_depths_rejected(recon_mod):
     from p265_amd import _lib
-    for bl, bc in ((12, 12), (10, 8), (8, 10)):
+    for bl, bc in ((13, 13), (14, 14), (12, 10), (10, 8), (8, 10)):
         params = R.make_params(pic_width=64, pic_height=64, bit_depth_luma=bl, bit_depth_chroma=bc)
         with pytest.raises(_lib.P265RError) as ei:
             recon_mod.ReconContext(params)
