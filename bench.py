@@ -853,7 +853,7 @@ def main(argv=None):
         "config": cfg,
         "roofline": {"bound": "hbm", "kernel": "intra_rows_kernel" if a.bit_depth == 8 else
                      ("intra_rows_kernel<..., uint16_t>" if a.bit_depth <= 10 else
-                      "intra_step_kernel<uint16_t> (one launch per anti-diagonal)"), "achieved": round(achieved, 2),
+                      "intra_rows_kernel<..., int16_t>"), "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": ("profiles/%s/summary.json (%s; rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE per launch)"
                                         % tuple(prof_tag.split(", ", 1))) if traffic else prof_tag,
@@ -866,8 +866,9 @@ def main(argv=None):
                               "achieved / avg_launch_ms: the 16-bit row pipeline (one workgroup per CU: twice the "
                               "LDS per wave), the batch alone (W = 12); the Main 10 path, not the headline "
                               "(DESIGN.md §4)" if a.bit_depth <= 10 else
-                              "achieved / avg_launch_ms of one anti-diagonal launch (BitDepth 11-12: the per-diagonal "
-                              "kernel, one workgroup per CTU of the diagonal); not the headline (DESIGN.md §4)")},
+                              "achieved / avg_launch_ms: the 16-bit row pipeline at BitDepth 11-12 (packed chroma "
+                              "angular sums split into 6-bit halves), the batch alone (W = 12); not the headline "
+                              "(DESIGN.md §4)")},
         "issue_rates": issue_rates(a.workload, "intra_rows_kernel", avg_launch_ms) if a.bit_depth == 8 else None,
         "intra_jobs_per_launch": {"luma": jl, "chroma": jch},
         "phases_ms_per_step": {k: round(acc[k] / a.steps, 4) for k in ("residual_ms", "intra_ms", "sao_ms", "total_ms")},
@@ -881,8 +882,7 @@ def main(argv=None):
     if w8:
         builds["w8_alone"] = {"avg_launch_ms": round(w8, 4),
                               "frac": round(bytes_per_launch / (w8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    if a.bit_depth <= 10:
-        out["roofline"]["builds"] = builds
+    out["roofline"]["builds"] = builds
     if a.workload == "c5":
         out["unit_latency_ms"] = c5_unit_latency(ctxs[0][0], cpu_sample, a.steps)
         if a.c5_world:

@@ -21,6 +21,7 @@
 // Same per-TB arithmetic as intra.h (8.4.4.2.x, 8.6.7); replaces decoder/intra.py:24-305
 // and decoder/reconstruction.py:4-27 driven by decoder/cu.py:595-615.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/p265r.h"
@@ -100,7 +101,7 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ lds_u8* lds8(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
 __device__ __forceinline__ lds_u32* lds32(uint32_t a) { return (lds_u32*)(uintptr_t)a; }
-// sample T (uint8_t, or uint16_t for BitDepth 9..10) at SAMPLE address s (byte address s * sizeof(T)): the
+// sample T (uint8_t, uint16_t for BitDepth 9..10, int16_t for 11..12) at SAMPLE address s (byte address s * sizeof(T)): the
 // job functions compute their LDS addresses in sample units, so one formula serves both sample sizes
 template <typename T>
 __device__ __forceinline__ __attribute__((address_space(3))) T* ldsT(uint32_t s) {
@@ -118,6 +119,21 @@ __device__ __forceinline__ uint32_t pmul(uint32_t w, uint32_t packed) {
         uint32_t r;
         asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(w * 0x00010001u), "v"(packed));
         return r;
+    }
+}
+
+// Packed angular interpolation ((32 - f) a + f b + 16) >> 5 of a Cb | Cr pair (wa + wb = 32).  BitDepth 11-12
+// (sample type int16_t, the row kernel's tag for them) passes 16 bits per half (32 x 4095), so each sample is
+// split into 6-bit halves a = 64 ah + al: the result is 2 (wa ah + wb bh) + ((wa al + wb bl + 16) >> 5)
+// exactly (64 X is a multiple of 32), every partial sum below 2^12 per half.
+template <typename T>
+__device__ __forceinline__ uint32_t pang(uint32_t wa, uint32_t a, uint32_t wb, uint32_t b) {
+    if constexpr (std::is_same<T, int16_t>::value) {
+        const uint32_t hi = pmul<T>(wa, (a >> 6) & 0x003f003fu) + pmul<T>(wb, (b >> 6) & 0x003f003fu);
+        const uint32_t lo = pmul<T>(wa, a & 0x003f003fu) + pmul<T>(wb, b & 0x003f003fu) + 0x00100010u;
+        return (hi << 1) + ((lo >> 5) & 0x003f003fu);
+    } else {
+        return ((pmul<T>(wa, a) + pmul<T>(wb, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
     }
 }
 
@@ -180,7 +196,7 @@ __device__ __forceinline__ uint32_t angtab_entry(int m, int p) {
     return a | b << 8 | (uint32_t)fact << 16 | (uint32_t)(32 - fact) << 24;
 }
 
-template <typename T>            // sample type: uint8_t (BitDepth 8), uint16_t (9..10)
+template <typename T>            // sample type: uint8_t (BitDepth 8), uint16_t (9..10), int16_t (11..12: a tag, pang)
 struct WaveLdsT {                // one wave's private CTU state (4564 B at 8 bits): a wave holds one row
     T        ref[2][136];        // unit at a time, luma OR chroma, so their areas overlap
     union {                      // ref: raw / final linear reference arrays
@@ -762,7 +778,7 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
         if (TAB) {                                             // AngTab4 entry (modes 10 / 26 included: fact 0)
             const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(angw & 0xffu), (int)v);
             const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((angw >> 8) & 0xffu), (int)v);
-            return ((pmul<T>(angw >> 24, a) + pmul<T>((angw >> 16) & 0xffu, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+            return pang<T>(angw >> 24, a, (angw >> 16) & 0xffu, b);
         }
         if (P265R_HV_FAST && (angw & 0xffu) == 0u)              // modes 10 / 26: a copy (no chroma smoothing)
             return ref(mode >= 18 ? 2 * n + 1 + x : 2 * n - 1 - y);
@@ -775,7 +791,7 @@ __device__ __forceinline__ uint32_t cpred(int mode, uint32_t angw, uint32_t v, i
         const int idx = pa >> 5, fact = pa & 31;
         const int nr0 = -1 - across - idx;
         const uint32_t a = ref(ang_ref<2 * n>(nr0, ia, ns)), b = ref(ang_ref<2 * n>(nr0 - 1, ia, ns));
-        return ((pmul<T>(32 - fact, a) + pmul<T>(fact, b) + 0x00100010u) >> 5) & 0x07ff07ffu;
+        return pang<T>(32 - fact, a, fact, b);
     }
     if (mode == 0) {
         const uint32_t lft = ref(2 * n - 1 - y), top = ref(2 * n + 1 + x);

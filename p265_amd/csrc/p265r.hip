@@ -463,13 +463,16 @@ int launch_rows(p265r_ctx* ctx, p265r_batch* b, hipStream_t st, bool alone) {
     // tile units, the decoder's small batches): W = 16, so every CTU row of a picture's chain can
     // be in flight at once (a 2-CTU-lag wavefront of 17 rows needs 17 waves; with 12 the rows
     // after the 12th wait for a whole row to finish)
-    // 16-bit samples (BitDepth 9..10): the same row pipeline on uint16_t LDS tiles and line buffers
+    // 16-bit samples (BitDepth 9..12): the same row pipeline on 16-bit LDS tiles and line buffers
     // (one workgroup per CU: twice the LDS of a wave); W = 12 alone, W = 8 beside other lanes' work
     if (ctx->geo.pel16) {
         // (wide pictures: W = 12 only while its two picture slots fit the 160 KB of LDS; p265r_create keeps
         // the per-diagonal schedule for pictures too wide for W = 8)
         int w = ctx->row_waves ? ctx->row_waves : (alone ? 12 : 8);
         if (w == 12 && rows_lds_bytes<uint16_t>(ctx->geo, 12, 2) > 160 * 1024) w = 8;
+        if (ctx->geo.bd[0] > 10)                    // BitDepth 11..12: int16_t tags the split angular sums (pang)
+            return w == 12 ? launch_rows_w<12, 1, false, false, int16_t>(ctx, b, st, alone)
+                           : launch_rows_w<8, 1, false, false, int16_t>(ctx, b, st, alone);
         return w == 12 ? launch_rows_w<12, 1, false, false, uint16_t>(ctx, b, st, alone)
                        : launch_rows_w<8, 1, false, false, uint16_t>(ctx, b, st, alone);
     }
@@ -557,9 +560,9 @@ int p265r_create(int device, const p265r_params* params, p265r_ctx** out) {
         if (std::getenv(k)) ctx->describe += std::string(ctx->describe.empty() ? "" : ", ") + "\"" + k + "\"";
     if (const char* v = std::getenv("P265R_SCHEDULE")) ctx->schedule = std::strcmp(v, "steps") == 0 ? 0 : 1;
     // 16-bit samples: the row pipeline while a W = 8 workgroup's LDS tiles and two line-buffer slots fit
-    // 160 KB (pictures up to ≈ 4K wide), else the per-diagonal kernel; BitDepth 11..12 always the latter
-    // (the row pipeline's packed Cb | Cr arithmetic needs every weighted chroma sum below 2^16)
-    if (g.pel16 && (p.bit_depth_luma > 10 || rows_lds_bytes<uint16_t>(g, 8, 2) > 160 * 1024)) ctx->schedule = 0;
+    // 160 KB (pictures up to ≈ 4K wide), else the per-diagonal kernel (BitDepth 11..12 too: the row kernel's
+    // packed Cb | Cr angular sums are split into 6-bit halves there, pang in intra_rows.h)
+    if (g.pel16 && rows_lds_bytes<uint16_t>(g, 8, 2) > 160 * 1024) ctx->schedule = 0;
     if (const char* v = std::getenv("P265R_SAO_ROWS")) ctx->sao_rows = std::atoi(v) == 2 ? 2 : (v[0] != '0' ? 1 : 0);
     if (const char* v = std::getenv("P265R_LUMA_LEAD")) ctx->luma_lead = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("P265R_SPLIT")) ctx->split = v[0] != '0';

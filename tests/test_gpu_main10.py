@@ -1,6 +1,7 @@
 """Main 10 (BitDepth 10) on the GPU through the C ABI vs the oracles, bit-exact.
 
-The 16-bit sample path (uint16_t planes; the row pipeline on uint16_t LDS tiles, intra_rows_kernel<..., uint16_t>,
+The 16-bit sample path (uint16_t planes; the row pipeline on 16-bit LDS tiles, intra_rows_kernel<..., uint16_t>
+(int16_t at BitDepth 11-12),
 and the per-diagonal kernel intra_step_kernel<uint16_t> (P265R_SCHEDULE=steps); sao16.h for SAO-only batches,
 loopfilter16.h; the residual kernels with bdShift = BitDepth + log2 - 5 and 20 - BitDepth) against
 oracle/recon_oracle.py (pinned at 10 bits by tests/golden/ref_components_bd10.npz from the reference's
@@ -137,11 +138,16 @@ def test_main10_row_pipeline_and_schedules(recon_mod, monkeypatch):
             np.testing.assert_array_equal(outs[i][c], ref[i][c], err_msg="steps pic %d c%d" % (i, c))
 
 
+@pytest.mark.parametrize("schedule", ["rows", "steps"])
 @pytest.mark.parametrize("bd", [11, 12])
 @pytest.mark.parametrize("case", ["uniform", "tiles", "sao_only", "ragged"])
-def test_high_bit_depth_per_diagonal(recon_mod, bd, case):
-    """BitDepth 11 / 12 (the per-diagonal kernel intra_step_kernel<uint16_t>, loopfilter16.h / sao16.h, the
-    residual kernels at bdShift BitDepth + log2 - 5 / 20 - BitDepth) against the oracles."""
+def test_high_bit_depth(recon_mod, monkeypatch, schedule, bd, case):
+    """BitDepth 11 / 12 against the oracles: the row pipeline (intra_rows_kernel<..., int16_t>: the packed
+    Cb | Cr angular sums split into 6-bit halves, pang) and the per-diagonal kernel intra_step_kernel<uint16_t>
+    (P265R_SCHEDULE=steps); loopfilter16.h / sao16.h; the residual kernels at bdShift BitDepth + log2 - 5 /
+    20 - BitDepth.  The synthetic pictures reach QpY 51 above 10 bits (Qp'Y up to 75: the uint16 deblocking map)."""
+    if schedule == "steps":
+        monkeypatch.setenv("P265R_SCHEDULE", "steps")
     if case == "ragged":
         big = R.make_params(pic_width=264, pic_height=200, ctb_log2_size=5, bit_depth_luma=bd, bit_depth_chroma=bd)
         pics = []
@@ -151,8 +157,8 @@ def test_high_bit_depth_per_diagonal(recon_mod, bd, case):
             pic.size = (w, h)
             pics.append(pic)
         with recon_mod.ReconContext(big) as ctx:
-            assert ctx.describe()["schedule"] == "steps"
-        _check(recon_mod, big, pics, "bd%d ragged" % bd)
+            assert ctx.describe()["schedule"] == schedule
+        _check(recon_mod, big, pics, "bd%d ragged %s" % (bd, schedule))
         return
     params = R.make_params(pic_width=200, pic_height=136, ctb_log2_size=5 if case != "uniform" else 6,
                            bit_depth_luma=bd, bit_depth_chroma=bd, loop_filter_across_tiles=0,
@@ -162,7 +168,9 @@ def test_high_bit_depth_per_diagonal(recon_mod, bd, case):
                          bypass_rate=0.05, pcm_rate=0.03, tskip_rate=0.3),
               sao_only=dict(perf=True, deblocking=False, tskip_rate=0.2, pcm_rate=0.02))[case]
     pics = [synth.make_picture(params, 5900 + bd + s, **kw) for s in range(2)]
-    _check(recon_mod, params, pics, "bd%d %s" % (bd, case))
+    with recon_mod.ReconContext(params) as ctx:
+        assert ctx.describe()["schedule"] == schedule
+    _check(recon_mod, params, pics, "bd%d %s %s" % (bd, case, schedule))
 
 
 def test_unsupported_bit_depths_rejected(recon_mod):
