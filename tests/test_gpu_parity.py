@@ -459,6 +459,25 @@ def test_invalid_chroma_size_and_tb_count_rejected(recon_mod):
             assert ei.value.code == _lib.EINVAL
 
 
+def test_unreferenced_tb_records_are_checked(recon_mod):
+    """Every TB of the array is packed, also one no CTU lists: its coefficient range and size are checked at
+    upload (ERANGE / EINVAL) instead of being read past the caller's coefficient array."""
+    from p265_amd import _lib
+    params = R.make_params(pic_width=64, pic_height=64)
+    pic = synth.make_picture(params, 3)
+    extra = np.zeros(1, R.TB_DTYPE)
+    extra["flags"] = R.TB_CBF
+    extra["log2_size"] = 5
+    for field, value, code in (("coef_off", len(pic.coef), _lib.ERANGE), ("log2_size", 7, _lib.EINVAL)):
+        e = extra.copy()
+        e[field] = value
+        bad = R.Picture(ctus=pic.ctus, tbs=np.concatenate([pic.tbs, e]), coef=pic.coef)
+        with recon_mod.ReconContext(params) as ctx:
+            with pytest.raises(_lib.P265RError) as ei:
+                ctx.upload([bad])
+            assert ei.value.code == code
+
+
 def test_chroma_sao_type_mismatch_rejected(recon_mod):
     """Cb and Cr share SaoTypeIdx and SaoEoClass (7.4.9.3.2): records that differ are EINVAL."""
     from p265_amd import _lib
