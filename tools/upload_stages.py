@@ -1,3 +1,9 @@
+"""Upload stage times of 512 synthetic 1080p pictures (the bench's PCIe-leg batch) on the GPU box.
+
+Needs an experiments build for the per-stage lines on stderr:
+  make variant V=exp FLAGS=-DP265R_EXPERIMENTS=1
+  P265R_LIB=p265_amd/libp265r_exp.so python tools/upload_stages.py
+"""
 import os, sys, time
 sys.path.insert(0, os.getcwd())
 os.environ.setdefault("P265R_UPLOAD_TIMES", "1")
