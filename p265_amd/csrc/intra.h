@@ -88,7 +88,7 @@ struct Geo {                    // batch-uniform geometry
                                 // wait and serves the left half of every CTU's bottom line from the half-CTU
                                 // publish alone (checks prep's `tr` and `br` deterministically); the prep kernel
                                 // checks `br` against the TBs' extents (error word bit 1)
-    int pel16;                  // samples are uint16_t (BitDepth 9..10, Main 10): planes of stride[] samples of 2
+    int pel16;                  // samples are 16-bit (BitDepth 9..12): planes of stride[] samples of 2
                                 // bytes, the per-diagonal intra kernel and loopfilter16.h (else uint8_t)
 };
 
@@ -137,7 +137,7 @@ __device__ __forceinline__ bool ctu_same_region(const p265r_ctu& a, const p265r_
     return a.slice_addr == b.slice_addr && a.tile_id == b.tile_id;
 }
 
-template <typename T>           // sample type: uint8_t (BitDepth 8) or uint16_t (BitDepth 9..10, Geo::pel16)
+template <typename T>           // sample type: uint8_t (BitDepth 8) or uint16_t (BitDepth 9..12, Geo::pel16)
 struct CtuLdsT {
     T        y[64 * 64];        // interior luma, stride 64
     T        c[2][32 * 32];     // interior chroma, stride 32

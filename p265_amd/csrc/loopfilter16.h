@@ -1,4 +1,4 @@
-// In-loop filters of the 16-bit sample path (BitDepth 9..10, Main 10; Geo::pel16): deblocking (8.7.2)
+// In-loop filters of the 16-bit sample path (BitDepth 9..12; Geo::pel16): deblocking (8.7.2)
 // + SAO (8.7.3) fused in one pass, as loopfilter.h does for 8-bit samples, with the bit-depth rules:
 //   beta = beta' * (1 << (BitDepthY - 8)), tC = tC' * (1 << (BitDepth - 8))   (8.7.2.5.3, 8.7.2.5.5)
 //   QpY = Qp'Y - QpBdOffsetY on both sides of an edge (the deblocking map carries Qp'Y, loopfilter.h)

@@ -1,4 +1,4 @@
-// SAO only (8.7.3) for 16-bit samples (BitDepth 9..10, Main 10), batches without deblocking: a
+// SAO only (8.7.3) for 16-bit samples (BitDepth 9..12), batches without deblocking: a
 // streaming strip kernel like sao_strip16.h, 8 samples (16 B) per lane.  One wave = one CTB row of one
 // component over a strip of 62 x 8 samples (lane l: the 8 samples at x = 496 s + 8 (l - 1); lanes 0 and
 // 63 only supply the neighbours of lanes 1 and 62); the wave walks down its CTB row with the rows above,

@@ -264,7 +264,7 @@ DEFAULTS = dict(
     frames=1, idr_period=0, log2_max_poc_lsb=8, poc_order=None, max_reorder=0,   # poc_order: POC per frame (IDR first)
     split_prob=0.55, tf_split_prob=0.5, nxn_prob=0.4, cbf_prob=0.7, chroma_cbf_prob=0.35, pcm_prob=0.08,
     bypass_prob=0.1, tskip_prob=0.3, density=0.25, big_prob=0.03,
-    bit_depth=8,                # BitDepthY = BitDepthC (8, or 9..10: Main 10 -- QpBdOffset, SAO cMax, PCM depths)
+    bit_depth=8,                # BitDepthY = BitDepthC (8, or 9..12 -- QpBdOffset, SAO cMax, PCM depths)
     scaling_lists=None,         # None | "default" (enabled, no lists coded) | "sps" (random lists in the SPS) |
                                 # "pps" (SPS lists overridden by random PPS lists)
 )
