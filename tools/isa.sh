@@ -7,7 +7,7 @@ mkdir -p "$(dirname "$out")"
 python3 - "$out" <<'PY'
 import re, sys
 txt = open(sys.argv[1]).read()
-for m in re.finditer(r'^(_Z\w*(?:intra_rows_kernel|sao_rows_kernel|sao_strip16_kernel|residual\w*_kernel|intra_prep_kernel|loopfilter_kernel|dbk_map_kernel|intra_step_kernel)\w*):[^\n]*\n(.*?)^\.Lfunc_end', txt, re.S | re.M):
+for m in re.finditer(r'^(_Z\w*(?:intra_rows_kernel|sao_rows_kernel|sao_strip16_kernel|sao16_strip_kernel|loopfilter16_kernel|residual\w*_kernel|intra_prep_kernel|loopfilter_kernel|dbk_map_kernel|intra_step_kernel)\w*):[^\n]*\n(.*?)^\.Lfunc_end', txt, re.S | re.M):
     name, code = m.group(1), m.group(2)
     k = re.search(r'\.amdhsa_kernel ' + name + r'\n(.*?)\.end_amdhsa_kernel', txt, re.S)
     body = k.group(1) if k else ''
